@@ -1,0 +1,411 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ FROM THE REFERENCE ITSELF.
+
+Run in the development container (needs /root/reference; never runs on the
+GPU box):
+
+    python tests/golden/gen_golden.py
+
+The reference (tfg.py) imports ``qsimov`` and ``mpi4py``, neither of which is
+installed.  This script makes it importable with
+* a RECORDING qsimov stand-in (QGate/QCircuit append their operations; no
+  simulation happens, ``Drewom.execute`` is never reached because the list
+  generator is replaced by injected lists), and
+* ``mpi4py.MPI`` backed by the package's in-process LocalWorld (comm.py), so
+  the reference's own ``QBA`` runs with all n+1 ranks as threads.
+
+Outputs (all small, committed):
+  gates.json          reference gate lists for n = 1..12 (tfg.py:15-65)
+  codec.json          measure_to_ints known answers (tfg.py:128-129)
+  consistent.json     consistent() known answers incl. edge cases (tfg.py:87-98)
+  protocol.json       decisions / V_i / accept counts of the reference QBA on
+                      injected lists, exact (CPython sets) and canonical
+                      (sorted sets) variants (tfg.py:309-363)
+  protocol_lists.npz  the injected lists, one array per case
+  logs.json/.npz      the five captured reference runs, parsed
+"""
+from __future__ import annotations
+
+import ast
+import importlib
+import json
+import os
+import re
+import sys
+import threading
+import types
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+REF = Path("/root/reference")
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "oracle"))
+
+import tfg_oracle as orc  # noqa: E402
+
+comm_mod = importlib.import_module("tfg---quantum-byzantine-agreement_amd.comm")
+
+
+# ---------------------------------------------------------------------------
+# import the reference with stand-ins for its two missing dependencies
+# ---------------------------------------------------------------------------
+def _install_stubs():
+    qs = types.ModuleType("qsimov")
+
+    class QGate:
+        def __init__(self, size, ancilla, name):
+            self.size, self.name, self.ops = size, name, []
+
+        def add_operation(self, gate, targets=None, controls=None, outputs=None):
+            self.ops.append((gate, targets, controls, outputs))
+
+    class QCircuit(QGate):
+        def __init__(self, size, csize, name):
+            super().__init__(size, 0, name)
+
+    class Drewom:
+        def execute(self, circuit):
+            raise RuntimeError("qsimov is not available; lists are injected")
+
+    qs.QGate, qs.QCircuit, qs.Drewom = QGate, QCircuit, Drewom
+    sys.modules["qsimov"] = qs
+    mpi_pkg = types.ModuleType("mpi4py")
+    mpi_pkg.MPI = comm_mod.local_mpi_module()
+    sys.modules["mpi4py"] = mpi_pkg
+    sys.modules["mpi4py.MPI"] = mpi_pkg.MPI
+    os.environ.setdefault("MPLBACKEND", "Agg")
+
+
+_install_stubs()
+sys.path.insert(0, str(REF))
+import tfg  # noqa: E402  (the reference)
+
+_real_np = np
+_tls = threading.local()
+
+
+class _NpProxy(types.ModuleType):
+    """``tfg.np`` replacement: numpy, except ``np.random`` is the calling rank's RandomState."""
+
+    def __getattr__(self, name):
+        if name == "random":
+            rs = getattr(_tls, "rs", None)
+            return rs if rs is not None else _real_np.random
+        return getattr(_real_np, name)
+
+
+tfg.np = _NpProxy("numpy_proxy")
+
+
+class SortedSet(set):
+    """A set whose iteration order is ascending: the 'canonical order' variant."""
+
+    def __iter__(self):
+        return iter(sorted(set.__iter__(self)))
+
+    def __repr__(self):
+        return "{" + ", ".join(map(repr, self)) + "}"
+
+
+# ---------------------------------------------------------------------------
+def gen_gates():
+    out = {}
+    for n in range(1, 13):
+        nq = orc.n_qubits(n)
+        g = tfg.notQCorrelated(n, nq)
+        notq = [[op[0], op[1], -1 if op[2] is None else op[2]] for op in g.ops]
+        circ = tfg.genNQCorrCircuit(n, nq)
+        q_cases = []
+        for seed in range(3):
+            _real_np.random.seed(1000 + seed)
+            gq = tfg.qCorrelated(n, nq)
+            _real_np.random.seed(1000 + seed)
+            rands = _real_np.arange(1, n + 1)
+            _real_np.random.shuffle(rands)
+            q_cases.append({
+                "seed": 1000 + seed,
+                "perm": [int(x) for x in rands],
+                "ops": [[op[0], op[1], -1 if op[2] is None else op[2]] for op in gq.ops],
+            })
+        meas = [[op[0], op[1], op[3]] for op in circ.ops[1:]]
+        out[str(n)] = {"nq": nq, "w": 2 ** nq, "size": (n + 1) * nq, "notq": notq,
+                       "q": q_cases, "measure": meas}
+    return out
+
+
+def gen_codec():
+    rng = _real_np.random.default_rng(7)
+    cases = []
+    for nq, size_l in [(1, 5), (2, 9), (3, 17), (4, 33), (4, 1)]:
+        raw = rng.integers(0, 2, nq * size_l).tolist()
+        cases.append({"nq": nq, "sizeL": size_l, "raw": raw,
+                      "ints": [int(x) for x in tfg.measure_to_ints(raw, size_l, nq)]})
+    return cases
+
+
+def gen_consistent():
+    cases = []
+
+    def add(v, L, w):
+        try:
+            res = bool(tfg.consistent(v, set(map(tuple, L)), w))
+            cases.append({"v": v, "L": [list(t) for t in L], "w": w, "result": res})
+        except Exception as exc:  # noqa: BLE001
+            cases.append({"v": v, "L": [list(t) for t in L], "w": w, "error": type(exc).__name__})
+
+    add(1, [], 4)                                   # StopIteration on an empty L
+    add(1, [()], 4)                                 # one empty tuple
+    add(1, [(), ()], 4)                             # set collapses duplicates
+    add(0, [(1, 2, 3)], 4)
+    add(2, [(1, 2, 3)], 4)                          # x == v
+    add(3, [(4, 1)], 4)                             # x == w is accepted (inclusive)
+    add(3, [(5, 1)], 4)                             # x > w
+    add(3, [(-1, 1)], 4)                            # x < 0
+    add(0, [(1, 2), (2, 1)], 4)
+    add(0, [(1, 2), (2, 2)], 4)                     # position collision
+    add(0, [(1, 2), (1, 3)], 4)
+    add(0, [(1, 2), (2, 3, 1)], 4)                  # ragged lengths
+    add(0, [(1,), (2,), (3,)], 4)
+    add(0, [(1,), (2,), (1,)], 4)                   # duplicate tuple collapses -> consistent
+    add(3, [(1, 2), (2, 1), (0, 0)], 4)             # 0 is allowed when v != 0
+    add(0, [(1, 2), (2, 1), (0, 3)], 4)
+    add(15, [(14, 2), (13, 1)], 16)
+    add(16, [(16, 2), (13, 1)], 16)                 # v == w
+    rng = _real_np.random.default_rng(11)
+    for _ in range(24):
+        w = int(rng.choice([2, 4, 8, 16]))
+        m = int(rng.integers(1, 5))
+        ln = int(rng.integers(0, 6))
+        v = int(rng.integers(0, w + 1))
+        L = [tuple(int(x) for x in rng.integers(0, w + 1, ln)) for _ in range(m)]
+        add(v, L, w)
+    return cases
+
+
+# ---------------------------------------------------------------------------
+# protocol fixtures: the reference's QBA on injected lists
+# ---------------------------------------------------------------------------
+def run_reference_qba(lists: np.ndarray, n_dis: int, seed: int, canonical: bool):
+    n = lists.shape[0] - 1
+    size_l = lists.shape[1]
+    nq = orc.n_qubits(n)
+    raw = orc.lists_to_raw(lists, nq)
+    per_rank = {r: {"accept": 0, "reject": 0, "sent": 0, "lines": []} for r in range(n + 1)}
+    real_consistent = tfg.consistent.__wrapped__ if hasattr(tfg.consistent, "__wrapped__") else tfg.consistent
+
+    def rank_of():
+        return comm_mod.current_comm().rank
+
+    def consistent(v, L, w):
+        ok = real_consistent(v, L, w)
+        per_rank[rank_of()]["accept" if ok else "reject"] += 1
+        return ok
+
+    consistent.__wrapped__ = real_consistent
+
+    def mpi_print(*args, **kwargs):
+        line = " ".join(str(a) for a in args)
+        per_rank[rank_of()]["lines"].append(line)
+        if "Sending" in line:
+            per_rank[rank_of()]["sent"] += 1
+
+    error_ranks = []
+    real_decide = tfg.decide_order
+
+    def decide_order(Vi, v, is_comm):
+        # The reference dies here (uncaught ValueError from min(set()), tfg.py:306)
+        # on every lieutenant whose V_i stayed empty.  Record which ranks would
+        # raise and let the run finish, so the fixture is deterministic.
+        try:
+            return real_decide(Vi, v, is_comm)
+        except ValueError:
+            error_ranks.append(rank_of())
+            return -1
+
+    saved = (tfg.consistent, tfg.mpi_print, tfg.generacionListas, tfg.decide_order)
+    tfg.decide_order = decide_order
+    tfg.consistent = consistent
+    tfg.mpi_print = mpi_print
+    tfg.generacionListas = lambda nParties, size, nQubits, w: raw.copy()
+    if canonical:
+        tfg.set = SortedSet
+    world = comm_mod.LocalWorld(n + 1, timeout=60.0)
+    vis = {}
+
+    def body(comm):
+        _tls.rs = _real_np.random.RandomState(seed * 1000 + comm.rank)
+        try:
+            tfg.QBA(size_l, n_dis)
+        finally:
+            _tls.rs = None
+
+    error = None
+    try:
+        world.run(body)
+    except Exception as exc:  # noqa: BLE001
+        error = type(exc).__name__
+    finally:
+        tfg.consistent, tfg.mpi_print, tfg.generacionListas, tfg.decide_order = saved
+        if canonical:
+            del tfg.set
+    if error is None and error_ranks:
+        error = "ValueError"
+    res = {"error": error, "error_ranks": sorted(error_ranks),
+           "messages": world.sent_messages, "bytes": world.sent_bytes}
+    lines0 = per_rank[0]["lines"]
+    for ln in lines0:
+        if ln.startswith("Decisions:"):
+            res["decisions"] = [int(x) for x in ln.split("[", 1)[1].rstrip("]").split()]
+        elif ln.startswith("Dishonests:"):
+            body_s = ln.split("[", 1)[1].rstrip("]").split()
+            res["dishonest"] = sorted(int(x) for x in body_s)
+        elif ln.startswith("Success:"):
+            res["success"] = ln.split()[-1] == "True"
+    res["V"] = {}
+    for r in range(2, n + 1):
+        for ln in per_rank[r]["lines"]:
+            m = re.match(rf"\[{r}\] V{r} = (.*)$", ln)
+            if m:
+                txt = m.group(1)
+                res["V"][str(r)] = [] if txt == "set()" else sorted(int(x) for x in re.findall(r"-?\d+", txt))
+    for ln in per_rank[1]["lines"]:
+        if ln.startswith("v ="):
+            res["v"] = int(ln.split("=")[1])
+    res["accept"] = [per_rank[r]["accept"] for r in range(n + 1)]
+    res["reject"] = [per_rank[r]["reject"] for r in range(n + 1)]
+    res["sent"] = [per_rank[r]["sent"] for r in range(n + 1)]
+    return res
+
+
+def tamper(lists: np.ndarray, rng, frac: float) -> np.ndarray:
+    out = lists.copy()
+    n1, sl = out.shape
+    w = orc.width(n1 - 1)
+    k = max(1, int(frac * sl))
+    pos = rng.integers(0, sl, k)
+    grp = rng.integers(2, n1, k)
+    out[grp, pos] = rng.integers(0, w, k)
+    return out
+
+
+def gen_protocol():
+    cases, arrays = [], {}
+    specs = []
+    for n in (3, 7, 11):
+        for size_l in (100, 1000):
+            for n_dis in (0, 1, 3):
+                for seed in range(2 if size_l == 1000 else 3):
+                    specs.append(("structured", n, size_l, n_dis, seed))
+    for n, size_l, n_dis, seed in [(3, 200, 1, 0), (7, 300, 2, 1), (11, 500, 3, 2), (5, 64, 1, 3), (2, 50, 0, 4)]:
+        specs.append(("tampered", n, size_l, n_dis, seed))
+        specs.append(("uniform", n, size_l, n_dis, seed))
+    for n, size_l, n_dis, seed in [(4, 120, 2, 5), (6, 90, 4, 6), (9, 333, 5, 7), (1, 40, 0, 8), (11, 1000, 5, 9)]:
+        specs.append(("structured", n, size_l, n_dis, seed))
+    for idx, (kind, n, size_l, n_dis, seed) in enumerate(specs):
+        rng = _real_np.random.default_rng(10_000 + idx)
+        if kind == "uniform":
+            lists = rng.integers(0, orc.width(n), (n + 1, size_l)).astype(np.uint8)
+        else:
+            lists = orc.closed_form_lists(n, size_l, rng)
+            if kind == "tampered":
+                lists = tamper(lists, rng, 0.02)
+        name = f"case{idx:03d}"
+        arrays[name] = lists
+        exact = run_reference_qba(lists, n_dis, seed, canonical=False)
+        canon = run_reference_qba(lists, n_dis, seed, canonical=True)
+        cases.append({"name": name, "kind": kind, "n": n, "sizeL": size_l, "nDishonest": n_dis,
+                      "seed": seed, "exact": exact, "canonical": canon})
+        print(f"{name} {kind:10s} n={n:2d} L={size_l:4d} dis={n_dis} -> exact {exact.get('decisions')} "
+              f"{exact.get('success')} {exact['error']} | canon {canon.get('decisions')} {canon.get('success')} {canon['error']}")
+    return cases, arrays
+
+
+# ---------------------------------------------------------------------------
+# the five captured reference runs
+# ---------------------------------------------------------------------------
+def _literal(txt: str):
+    return ast.literal_eval(txt.replace("set()", "()"))
+
+
+def parse_log(path: Path):
+    lines = path.read_text().splitlines()
+    info = {"file": path.name, "packets": [], "own_L": {}, "V": {}, "actions": []}
+    lists = {}
+    for ln in lines:
+        m = re.match(r"\[(\d+)\]: (Lc|L\d+) = (\[.*\])$", ln)
+        if m:
+            r, name = int(m.group(1)), m.group(2)
+            vals = ast.literal_eval(m.group(3))
+            if name == "Lc":
+                lists[1] = vals           # rank 1's Lc = group 1
+            elif r == 1:
+                lists[0] = vals           # rank 1's Li = group 0
+            else:
+                lists[r] = vals
+            continue
+        m = re.match(r"^(?:w|\|W\|) = (\d+)$", ln)
+        if m:
+            info["w"] = int(m.group(1))
+            continue
+        if ln.startswith("isQCorr ="):
+            info["isQCorr_order"] = list(_literal(ln.split("=", 1)[1].strip()))
+            continue
+        m = re.match(r"^v = (\d+)$", ln)
+        if m:
+            info["v"] = int(m.group(1))
+            continue
+        m = re.match(r"\[(B?)(\d+) -> (\d+)\] Sending (\(.*\))$", ln)
+        if m:
+            P, (v, L) = _literal(m.group(4))
+            P = list(P) if not isinstance(P, tuple) else list(P)
+            info["packets"].append({"src": int(m.group(2)), "dst": int(m.group(3)), "bad": m.group(1) == "B",
+                                    "P_order": [int(x) for x in P], "v": int(v),
+                                    "L": [list(map(int, t)) for t in (L if L != () else [])]})
+            continue
+        m = re.match(r"\[(\d+)\] L = (\{.*\})$", ln)
+        if m:
+            info["own_L"][m.group(1)] = [list(map(int, t)) for t in _literal(m.group(2))]
+            continue
+        m = re.match(r"\[(\d+)\] V(\d+) = (.*)$", ln)
+        if m:
+            txt = m.group(3)
+            info["V"][m.group(1)] = [] if txt == "set()" else sorted(int(x) for x in re.findall(r"\d+", txt))
+            continue
+        if ln.startswith("The action for general"):
+            info["actions"].append(ln)
+            continue
+        if ln.startswith("Decisions:"):
+            info["decisions"] = [int(x) for x in ln.split("[", 1)[1].rstrip("]").split()]
+        elif ln.startswith("Dishonests:"):
+            info["dishonest"] = sorted(int(x) for x in ln.split("[", 1)[1].rstrip("]").split())
+        elif ln.startswith("Success:"):
+            info["success"] = ln.split()[-1] == "True"
+    n = max(lists)
+    info["n"] = n
+    arr = np.array([lists[g] for g in range(n + 1)], dtype=np.uint8)
+    return info, arr
+
+
+def main():
+    outdir = HERE
+    (outdir / "gates.json").write_text(json.dumps(gen_gates()))
+    (outdir / "codec.json").write_text(json.dumps(gen_codec()))
+    (outdir / "consistent.json").write_text(json.dumps(gen_consistent(), indent=0))
+    logs, log_arrays = [], {}
+    for p in sorted((REF / "logs tests").glob("*.txt")):
+        info, arr = parse_log(p)
+        logs.append(info)
+        log_arrays[p.stem] = arr
+    (outdir / "logs.json").write_text(json.dumps(logs))
+    np.savez_compressed(outdir / "logs.npz", **log_arrays)
+    cases, arrays = gen_protocol()
+    (outdir / "protocol.json").write_text(json.dumps(cases, indent=0))
+    np.savez_compressed(outdir / "protocol_lists.npz", **arrays)
+    print("wrote", sorted(x.name for x in outdir.iterdir()))
+
+
+if __name__ == "__main__":
+    main()
