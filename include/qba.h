@@ -1,0 +1,159 @@
+/*
+ * qba.h -- C ABI of libqba.so, the MI355X (gfx950) engine for the data-parallel
+ * core of the quantum Byzantine agreement protocol of
+ * Carl0sGV/TFG---Quantum-Byzantine-Agreement (tfg.py).
+ *
+ * The reference has no plugin/operator API; its hot path
+ * sits behind (1) the qsimov gate/executor calls and (2) four module-level
+ * functions plus four inline comprehensions.  Each entry point below names
+ * the reference interface it replaces.  INTEGRATION.md shows the ctypes
+ * binding a maintainer of tfg.py would add.
+ *
+ * Conventions
+ *   - Every function returns QBA_OK (0) or a negative qba_status; the message
+ *     of the last failure on the calling thread is qba_last_error().  No C++
+ *     exception crosses this boundary.
+ *   - All array arguments named *_dev are DEVICE pointers allocated by the
+ *     caller (e.g. torch tensors' data_ptr()); *_host are host pointers.
+ *   - `stream` is a hipStream_t (NULL = the legacy default stream).  Work is
+ *     enqueued asynchronously; functions documented as "synchronous" wait.
+ *   - One qba_ctx per device; a ctx is not thread-safe (one host thread, or
+ *     external locking).  The ctx owns only its scratch and compiled
+ *     resource programs.
+ *   - Lists are uint8 matrices lists[g][k] with row stride `ld` bytes:
+ *     row g = measured group g (row 0 is what rank 1 calls Li, row 1 is Lc,
+ *     row g>=2 is party g's list).  ld % 4 == 0 and the base
+ *     pointer must be 4-byte aligned.
+ *   - Count tensors are int64:  H[u][g][x] (w x (n+1) x w),
+ *     C[u][g][h] ((w x (n+1) x (n+1)), symmetric, diagonal = |P_u|),
+ *     P[u] = |P_u| (w).  Only Q-correlated positions (L0[k] != L1[k],
+ *     tfg.py:327) are counted, binned by u = L1[k] (= Lc[k], tfg.py:182).
+ */
+#ifndef QBA_H
+#define QBA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__) || defined(__clang__)
+#define QBA_API __attribute__((visibility("default")))
+#else
+#define QBA_API
+#endif
+
+typedef struct qba_ctx qba_ctx;
+typedef void *qba_stream; /* hipStream_t */
+
+typedef enum qba_status {
+  QBA_OK = 0,
+  QBA_EINVAL = -1,      /* bad argument */
+  QBA_EHIP = -2,        /* HIP runtime failure */
+  QBA_ENOMEM = -3,      /* device allocation failed */
+  QBA_EUNSUPPORTED = -4,/* outside the supported envelope (e.g. n > 15) */
+  QBA_ESTATE = -5       /* e.g. no resource program compiled for this n */
+} qba_status;
+
+enum { QBA_KIND_NOTQ = 0, QBA_KIND_Q = 1 };
+enum { QBA_GATE_H = 0, QBA_GATE_X = 1 }; /* gate triples: {kind, target, control|-1} */
+
+#define QBA_MAX_PARTIES 15 /* w <= 16: one nibble per group in the 64-bit outcome */
+
+/* ---- library / context ---------------------------------------------------------- */
+QBA_API const char *qba_last_error(void);
+QBA_API int qba_version(void); /* major*10000 + minor*100 + patch */
+QBA_API int qba_init(int device, qba_ctx **out);
+QBA_API int qba_destroy(qba_ctx *ctx);
+/* Pre-allocate scratch for counts launches of up to `max_blocks` workgroups so
+ * that later calls never allocate (required before hipGraph capture). */
+QBA_API int qba_reserve(qba_ctx *ctx, int n_parties, int64_t max_blocks);
+
+/* ---- (A1/A2) resource preparation: dense fp64 statevector, gfx950 kernels --------- */
+/* Replaces qs.QGate(...).add_operation(...) + qs.Drewom().execute(...) state
+ * preparation (tfg.py:15-65, 76, 80).  Qubit 0 is the MSB of a basis index. */
+QBA_API int qba_sv_init(qba_ctx *ctx, double *sv_dev, int nqubits, qba_stream stream);
+QBA_API int qba_sv_apply(qba_ctx *ctx, double *sv_dev, int nqubits, const int32_t *gates_host,
+                 int n_gates, qba_stream stream);
+/* Probabilities |a_i|^2 > eps, compacted in ascending index order.  Writes at
+ * most `cap` (index, prob) pairs; *count_host receives the full support size.
+ * Synchronous. */
+QBA_API int qba_sv_support(qba_ctx *ctx, const double *sv_dev, int nqubits, double eps,
+                   int64_t *idx_dev, double *prob_dev, int64_t cap, int64_t *count_host,
+                   qba_stream stream);
+/* Compile one of the two circuits of an n-party run into the sampler's
+ * factored alias-table program.  `gates_host` is the reference's gate list
+ * for that circuit (notQCorrelated, tfg.py:15-22, or qCorrelated, tfg.py:25-40);
+ * for QBA_KIND_Q, `perm_host[g-1]` is the permutation the list was built
+ * with: its X gates are verified to be the classical mask the sampler draws
+ * afresh per entry.  The circuit is split into entangled registers, each is
+ * simulated on the device, its support compacted and turned into an alias
+ * table.  Synchronous. */
+QBA_API int qba_resource_compile(qba_ctx *ctx, int n_parties, int kind, const int32_t *gates_host,
+                         int n_gates, const int32_t *perm_host);
+/* Export the compiled program for kind (for tests / the CPU twin):
+ * factor descriptors (bits, uniform, table offset, u-word) and the tables. */
+QBA_API int qba_program_export(qba_ctx *ctx, int n_parties, int kind, int32_t *n_factors,
+                       int32_t *desc_host /* [16][6] */, uint64_t *pat_host,
+                       uint64_t *apat_host, uint64_t *thr_host, int32_t table_cap,
+                       int32_t *table_len);
+
+/* ---- (A3/A4) Born sampling: Philox4x32-10 keyed by the GLOBAL entry index -------- */
+/* Replaces generacionListas (tfg.py:68-84) + measure_to_ints (tfg.py:128-129):
+ * writes lists[g][k - first] for entries k in [first, first+count). */
+QBA_API int qba_sample(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first, uint64_t count,
+               uint8_t *lists_dev, uint64_t ld, qba_stream stream);
+
+/* ---- (A5-A8) checks, count mode -------------------------------------------------- */
+/* One pass over the lists computing H, C, P (see conventions); replaces the
+ * per-packet work of tfg.py:182, 189, 291-294, 327 and consistent() 87-98 in
+ * canonical order.  accumulate != 0 adds into H/C/P instead of overwriting. */
+QBA_API int qba_check_counts(qba_ctx *ctx, int n_parties, const uint8_t *lists_dev, uint64_t count,
+                     uint64_t ld, int64_t *H_dev, int64_t *C_dev, int64_t *P_dev,
+                     int accumulate, qba_stream stream);
+/* Statistics of the last counts launch on this ctx (synchronous):
+ * out[0] = Q-correlated entries that held a value >= w and were therefore
+ * not counted (never happens for lists from qba_sample), out[1] reserved. */
+QBA_API int qba_last_stats(qba_ctx *ctx, int64_t *out2_host);
+/* Fused sample + check: lists are written once and counted from registers. */
+QBA_API int qba_sample_check(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
+                     uint64_t count, uint8_t *lists_dev, uint64_t ld, int64_t *H_dev,
+                     int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);
+
+/* ---- (A5-A8) checks, exact-order mode (bit-exact protocol parity) --------------- */
+/* isQCorrList = {k : Li[k] != Lc[k]} (tfg.py:327) as ascending indices.
+ * *count_host receives the number found; at most `cap` are written. Synchronous. */
+QBA_API int qba_isq_indices(qba_ctx *ctx, const uint8_t *li_dev, const uint8_t *lc_dev, uint64_t count,
+                    int64_t *idx_dev, int64_t cap, int64_t *count_host, qba_stream stream);
+/* P = {x in order : Lc[x] == v} keeping the order of `order` (tfg.py:182).
+ * Synchronous. */
+QBA_API int qba_select_eq(qba_ctx *ctx, const int64_t *order_dev, int64_t m, const uint8_t *lc_dev,
+                  int64_t v, int64_t *out_dev, int64_t *count_host, qba_stream stream);
+/* tuple(Li[j] for j in P) in the given order (tfg.py:189, 291). */
+QBA_API int qba_gather(qba_ctx *ctx, const uint8_t *li_dev, uint64_t list_len, const int64_t *idx_dev,
+               int64_t m, int64_t *out_dev, qba_stream stream);
+/* consistent(v, L, w) conditions 2 and 3 (tfg.py:93-98) over m equal-length
+ * tuples stored row-major [m][len] (Cond1 and the empty-L StopIteration stay
+ * on the host).  *ok_host = 1 if consistent.  Synchronous. */
+QBA_API int qba_consistent(qba_ctx *ctx, const int64_t *tuples_dev, int64_t m, int64_t len, int64_t v,
+                   int64_t w, int32_t *ok_host, qba_stream stream);
+
+/* ---- wire-compatible codec (rawS layout, tfg.py:81-84, 128-129, 142-161) -------- */
+QBA_API int qba_bits_to_values(qba_ctx *ctx, const int64_t *raw_dev, uint64_t count, int nq,
+                       uint8_t *values_dev, qba_stream stream);
+QBA_API int qba_values_to_bits(qba_ctx *ctx, const uint8_t *values_dev, uint64_t count, int nq,
+                       int64_t *raw_dev, qba_stream stream);
+
+/* ---- helpers exported for tests ------------------------------------------------- */
+/* Vose alias table over k probabilities (host): thr[i] in [0, 2^32] (2^32 =
+ * always keep column i), alias[i] = column taken otherwise. */
+QBA_API int qba_alias_build(const double *prob_host, int32_t k, uint64_t *thr_host, int32_t *alias_host);
+/* Philox4x32-10 on the device for KATs: out[4*i..] = philox(ctr_i, key). */
+QBA_API int qba_philox_dev(qba_ctx *ctx, const uint32_t *ctr_dev, int64_t n, uint64_t key,
+                   uint32_t *out_dev, qba_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QBA_H */

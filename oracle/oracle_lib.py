@@ -1,0 +1,86 @@
+"""ctypes loader of oracle/lib/liboracle.so (the C twin in sampler_ref.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg; never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+LIB = Path(__file__).resolve().parent / "lib" / "liboracle.so"
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            raise FileNotFoundError(f"{LIB} missing: run `make -C oracle`")
+        _lib = C.CDLL(str(LIB))
+        _lib.oracle_counts.restype = C.c_int64
+        _lib.oracle_sample_counts.restype = C.c_int64
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data)
+
+
+def n_qubits(n: int) -> int:
+    return int(n).bit_length()
+
+
+def philox(ctr: np.ndarray, key: int) -> np.ndarray:
+    ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
+    out = np.zeros_like(ctr)
+    lib().oracle_philox(_p(ctr), C.c_int64(len(ctr)), C.c_uint64(key), _p(out))
+    return out
+
+
+def _prog_args(prog: dict):
+    desc = np.ascontiguousarray(prog["desc"], dtype=np.int32)
+    pat = np.ascontiguousarray(prog["pat"], dtype=np.uint64)
+    apat = np.ascontiguousarray(prog["apat"], dtype=np.uint64)
+    thr = np.ascontiguousarray(prog["thr"], dtype=np.uint64)
+    keep = (desc, pat, apat, thr)
+    return keep, [C.c_int(int(prog["nfac"])), _p(desc), _p(pat), _p(apat), _p(thr)]
+
+
+def sample(n: int, seed: int, first: int, count: int, prog_notq: dict, prog_q: dict) -> np.ndarray:
+    lists = np.zeros((n + 1, max(count, 1)), np.uint8)
+    k0, a0 = _prog_args(prog_notq)
+    k1, a1 = _prog_args(prog_q)
+    lib().oracle_sample(C.c_int(n), C.c_uint64(seed), C.c_uint64(first), C.c_uint64(count), *a0, *a1,
+                        _p(lists), C.c_uint64(lists.shape[1]))
+    return lists[:, :count]
+
+
+def counts(lists: np.ndarray, n: int):
+    lists = np.ascontiguousarray(lists, dtype=np.uint8)
+    w = 1 << n_qubits(n)
+    H = np.zeros((w, n + 1, w), np.int64)
+    Cc = np.zeros((w, n + 1, n + 1), np.int64)
+    P = np.zeros(w, np.int64)
+    bad = lib().oracle_counts(C.c_int(n), _p(lists), C.c_uint64(lists.shape[1]),
+                              C.c_uint64(lists.shape[1]), _p(H), _p(Cc), _p(P))
+    return H, Cc, P, int(bad)
+
+
+def sample_counts(n: int, seed: int, first: int, count: int, prog_notq: dict, prog_q: dict):
+    lists = np.zeros((n + 1, max(count, 1)), np.uint8)
+    w = 1 << n_qubits(n)
+    H = np.zeros((w, n + 1, w), np.int64)
+    Cc = np.zeros((w, n + 1, n + 1), np.int64)
+    P = np.zeros(w, np.int64)
+    k0, a0 = _prog_args(prog_notq)
+    k1, a1 = _prog_args(prog_q)
+    lib().oracle_sample_counts(C.c_int(n), C.c_uint64(seed), C.c_uint64(first), C.c_uint64(count),
+                               *a0, *a1, _p(lists), C.c_uint64(lists.shape[1]), _p(H), _p(Cc), _p(P))
+    return lists[:, :count], H, Cc, P
+
+
+def threads() -> int:
+    return int(lib().oracle_threads())

@@ -269,7 +269,7 @@ def run_reference_qba(lists: np.ndarray, n_dis: int, seed: int, canonical: bool)
         for ln in per_rank[r]["lines"]:
             m = re.match(rf"\[{r}\] V{r} = (.*)$", ln)
             if m:
-                txt = m.group(1)
+                txt = re.sub(r"np\.int64\((-?\d+)\)", r"\1", m.group(1))
                 res["V"][str(r)] = [] if txt == "set()" else sorted(int(x) for x in re.findall(r"-?\d+", txt))
     for ln in per_rank[1]["lines"]:
         if ln.startswith("v ="):

@@ -1,0 +1,287 @@
+"""GPU parity of the HIP kernels against the oracle (C twin + numpy restatement)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib
+import statevector as sv_oracle
+import tfg_oracle as orc
+from conftest import GOLDEN, sub
+
+pytestmark = pytest.mark.gpu
+
+KATS = [
+    ([0, 0, 0, 0], 0, [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]),
+    ([0xFFFFFFFF] * 4, 0xFFFFFFFFFFFFFFFF, [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]),
+    ([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], 0x299F31D0A4093822,
+     [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]),
+]
+
+
+def test_philox_device_kat(engine):
+    for ctr, key, want in KATS:
+        assert list(engine.philox(np.array(ctr, np.uint32), key)[0]) == want
+    rng = np.random.default_rng(1)
+    ctr = rng.integers(0, 2 ** 32, (4096, 4), dtype=np.uint64).astype(np.uint32)
+    key = 0x0123456789ABCDEF
+    assert np.array_equal(engine.philox(ctr, key), oracle_lib.philox(ctr, key))
+
+
+def _program_distribution(prog, N):
+    """Full outcome distribution of a compiled program (product of its factors)."""
+    dist = {0: 1.0}
+    for f in range(prog["nfac"]):
+        bits, uniform, off = prog["desc"][f][:3]
+        K = 1 << bits
+        col_p = {}
+        for c in range(K):
+            thr = int(prog["thr"][off + c])
+            keep = 1.0 if uniform else thr / 2 ** 32
+            for pat, p in ((int(prog["pat"][off + c]), keep), (int(prog["apat"][off + c]), 1 - keep)):
+                if p > 0:
+                    col_p[pat] = col_p.get(pat, 0.0) + p / K
+        new = {}
+        for a, pa in dist.items():
+            for b, pb in col_p.items():
+                new[a ^ b] = new.get(a ^ b, 0.0) + pa * pb
+        dist = new
+    return dist
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5])
+def test_program_matches_reference_statevector(engine, n):
+    """Compiled tables == probabilities of the reference's own gate lists (gates.json)."""
+    gates = json.loads((GOLDEN / "gates.json").read_text())[str(n)]
+    N = gates["size"]
+    info = engine.prepare(n)
+    # not-Q circuit
+    ops = [(g, t, c) for g, t, c in gates["notq"]]
+    probs = sv_oracle.probabilities(sv_oracle.run(ops, N))
+    dist = _program_distribution(info["notq"], N)
+    idx = np.nonzero(probs > 1e-30)[0]
+    assert sorted(dist) == sorted(int(i) for i in idx)
+    for i in idx:
+        assert abs(dist[int(i)] - probs[i]) < 1e-12
+    # Q circuit: every recorded permutation; the program is pi-free, the mask is
+    # the permutation layout the sampler draws
+    nq = gates["nq"]
+    for case in gates["q"]:
+        ops = [(g, t, c) for g, t, c in case["ops"]]
+        probs = sv_oracle.probabilities(sv_oracle.run(ops, N))
+        mask = sum(int(v) << (N - (g + 1) * nq) for g, v in enumerate(case["perm"], start=1))
+        dist = _program_distribution(info["q"], N)
+        idx = np.nonzero(probs > 1e-30)[0]
+        assert sorted(a ^ mask for a in dist) == sorted(int(i) for i in idx)
+        for a, p in dist.items():
+            assert abs(p - probs[a ^ mask]) < 1e-12
+
+
+@pytest.mark.parametrize("n", [6, 7, 8, 11, 12, 15])
+def test_program_registers_large_n(engine, n):
+    """Per-factor check at sizes where the full state does not fit: the program's
+    marginal over each group equals the closed form (A1/A2)."""
+    info = engine.prepare(n)
+    nq, w = engine.sizes(n)
+    N = (n + 1) * nq
+    for kind in ("notq", "q"):
+        prog = info[kind]
+        total_bits = sum(int(d[0]) for d in prog["desc"])
+        assert all(int(d[1]) == 1 for d in prog["desc"]), "H/X/CX resources are uniform"
+        if kind == "q":
+            assert total_bits == nq  # the GHZ registers: L_g = r for all g
+            pats = set(int(p) for p in prog["pat"])
+            want = {sum(r << (N - (g + 1) * nq) for g in range(n + 1)) for r in range(w)}
+            assert pats == want
+        else:
+            assert total_bits == n * nq  # L0 = L1 and L1..Ln free
+
+
+@pytest.mark.parametrize("n,first,count", [(1, 0, 1001), (2, 7, 999), (3, 0, 4096), (5, 3, 777),
+                                           (7, 1 << 33, 5003), (11, 0, 100_003), (11, (1 << 40) + 5, 20_001),
+                                           (13, 99, 3000), (15, 1, 8191)])
+def test_sampler_bit_exact(engine, n, first, count):
+    seed = 0x5EED ^ (n << 20)
+    info = engine.prepare(n)
+    lists = engine.sample(n, seed, first, count)
+    torch.cuda.synchronize()
+    got = lists[:, :count].cpu().numpy()
+    ref = oracle_lib.sample(n, seed, first, count, info["notq"], info["q"])
+    assert np.array_equal(got, ref)
+
+
+def test_shard_invariance(engine):
+    """Lists depend only on the global entry index: any split gives the same bytes."""
+    n, seed, total = 11, 77, 50_000
+    full = engine.sample(n, seed, 0, total)[:, :total].cpu().numpy()
+    cuts = [0, 1, 4097, 12_345, 33_333, total]
+    parts = [engine.sample(n, seed, a, b - a)[:, : b - a].cpu().numpy() for a, b in zip(cuts, cuts[1:])]
+    assert np.array_equal(np.concatenate(parts, axis=1), full)
+
+
+def test_structure_and_chi2(engine):
+    """At Q positions all n+1 values are distinct and L_g XOR L_1 is a permutation
+    pattern; elsewhere L0 == L1; marginals uniform (chi-square)."""
+    from scipy import stats
+    n, count = 11, 2_000_000
+    nq, w = engine.sizes(n)
+    L = engine.sample(n, 2024, 0, count)[:, :count].cpu().numpy().astype(np.int64)
+    q = L[0] != L[1]
+    frac = q.mean()
+    assert abs(frac - 0.5) < 5 * np.sqrt(0.25 / count)
+    Lq = L[:, q]
+    srt = np.sort(Lq, axis=0)
+    assert (np.diff(srt, axis=0) != 0).all()
+    x = Lq[1:] ^ Lq[0]  # pi(g) for g = 1..n
+    assert np.array_equal(np.sort(x, axis=0), np.repeat(np.arange(1, n + 1)[:, None], x.shape[1], 1))
+    for g in range(n + 1):
+        cnt = np.bincount(L[g], minlength=w)
+        assert stats.chisquare(cnt).pvalue > 1e-4
+    # pi(1) uniform over 1..n at Q positions, pairs (L2, L3) independent at non-Q
+    assert stats.chisquare(np.bincount(x[0], minlength=n + 1)[1:]).pvalue > 1e-4
+    nonq = L[:, ~q]
+    joint = np.bincount(nonq[2] * w + nonq[3], minlength=w * w)
+    assert stats.chisquare(joint).pvalue > 1e-4
+
+
+@pytest.mark.parametrize("n,count", [(3, 10_001), (7, 40_000), (11, 123_457), (15, 5000)])
+def test_counts_match_oracle(engine, n, count):
+    seed = 99 + n
+    info = engine.prepare(n)
+    lists, c_fused = engine.sample_check(n, seed, 5, count)
+    c_sep = engine.check_counts(lists, n, count)
+    torch.cuda.synchronize()
+    ref_lists = oracle_lib.sample(n, seed, 5, count, info["notq"], info["q"])
+    H, C, P, bad = oracle_lib.counts(ref_lists, n)
+    assert bad == 0
+    for c in (c_fused, c_sep):
+        gH, gC, gP = c.numpy()
+        assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+    # numpy restatement agrees as well
+    H2, C2, P2 = orc.counts(ref_lists, n)
+    assert np.array_equal(H2, H) and np.array_equal(C2, C) and np.array_equal(P2, P)
+
+
+def test_counts_on_fixture_lists(engine):
+    """Count mode on the injected fixture lists, incl. tampered / uniform ones with
+    collisions (slow path) -- against the numpy restatement."""
+    arrays = np.load(GOLDEN / "protocol_lists.npz")
+    for name in arrays.files:
+        L = arrays[name]
+        n = L.shape[0] - 1
+        d = torch.zeros((n + 1, (L.shape[1] + 63) // 64 * 64), dtype=torch.uint8, device=engine.device)
+        d[:, : L.shape[1]] = torch.from_numpy(L)
+        c = engine.check_counts(d, n, L.shape[1])
+        gH, gC, gP = c.numpy()
+        H, C, P = orc.counts(L, n)
+        assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P), name
+
+
+def test_counts_accumulate_and_invalid(engine):
+    n, count = 7, 10_000
+    lists = engine.sample(n, 5, 0, count)
+    a = engine.check_counts(lists, n, count)
+    b = engine.check_counts(lists, n, count, counts=engine.alloc_counts(n))
+    engine.check_counts(lists, n, count, counts=b, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(b.H, 2 * a.H) and torch.equal(b.C, 2 * a.C) and torch.equal(b.P, 2 * a.P)
+    bad = lists.clone()
+    q = (bad[0, :count] != bad[1, :count]).nonzero()[:3, 0]
+    bad[5, q] = 200
+    engine.check_counts(bad, n, count)
+    assert engine.last_stats()[0] == 3
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5])
+def test_full_statevector_vs_oracle(engine, n):
+    gates = json.loads((GOLDEN / "gates.json").read_text())[str(n)]
+    N = gates["size"]
+    for ops in [gates["notq"]] + [c["ops"] for c in gates["q"]]:
+        trip = np.array([(0 if g == "H" else 1, t, c) for g, t, c in ops], np.int32)
+        sv = engine.statevector(N, trip)
+        torch.cuda.synchronize()
+        ref = sv_oracle.run([tuple(o) for o in ops], N)
+        assert np.max(np.abs(sv.cpu().numpy() - ref)) < 1e-12
+        idx, prob = engine.support(sv, N)
+        ridx, rprob = sv_oracle.support(sv_oracle.probabilities(ref), 1e-24)
+        assert np.array_equal(idx, ridx) and np.max(np.abs(prob - rprob)) < 1e-12
+
+
+def test_ghz_register_statevector(engine):
+    """One entangled register of the Q resource (n+1 qubits) at n=19: support
+    {0...0, 1...1}, each 1/2 (the per-register closed form of A2)."""
+    q = 20
+    trip = np.array([(0, 0, -1)] + [(1, t, 0) for t in range(1, q)], np.int32)
+    sv = engine.statevector(q, trip)
+    idx, prob = engine.support(sv, q)
+    assert list(idx) == [0, (1 << q) - 1]
+    assert np.max(np.abs(prob - 0.5)) < 1e-12
+
+
+def test_exact_mode_kernels(engine):
+    rng = np.random.default_rng(3)
+    for count in (1, 17, 1000, 70_001):
+        l0 = rng.integers(0, 4, count).astype(np.uint8)
+        l1 = np.where(rng.random(count) < 0.5, l0, rng.integers(0, 4, count)).astype(np.uint8)
+        d0, d1 = engine.to_device(l0), engine.to_device(l1)
+        assert np.array_equal(engine.isq_indices(d0, d1), orc.is_qcorr_indices(l0, l1))
+        order = rng.permutation(count).astype(np.int64)
+        for v in range(4):
+            assert engine.select_eq(order, d1, v).tolist() == orc.p_filter(order, l1, v)
+        idx = rng.integers(0, count, min(count, 500)).astype(np.int64)
+        assert tuple(engine.gather(d0, idx)) == orc.gather(l0, idx)
+    with pytest.raises(sub("_lib").QbaError):
+        engine.gather(d0, np.array([count], np.int64))
+
+
+def test_consistent_kernel_kat(engine):
+    """qba_consistent + host Cond1 == the reference's consistent() on its KAT table."""
+    for case in json.loads((GOLDEN / "consistent.json").read_text()):
+        tuples = list({tuple(t) for t in case["L"]})
+        if not tuples:
+            assert case.get("error") == "StopIteration"
+            continue
+        lens = {len(t) for t in tuples}
+        if len(lens) > 1:
+            got = False
+        else:
+            got = engine.consistent_rows(np.array(tuples, np.int64).reshape(len(tuples), -1),
+                                         case["v"], case["w"])
+        assert got == case["result"], case
+
+
+def test_codec_kat(engine):
+    for case in json.loads((GOLDEN / "codec.json").read_text()):
+        raw = engine.to_device(np.array(case["raw"], np.int64))
+        vals = engine.bits_to_values(raw, case["sizeL"], case["nq"]).cpu().numpy()
+        assert vals.tolist() == case["ints"]
+        back = engine.values_to_bits(engine.to_device(vals), case["sizeL"], case["nq"]).cpu().numpy()
+        assert back.tolist() == case["raw"]
+
+
+def test_log_tuples_exact_order(engine):
+    """The reference's own captured runs (logs tests/): every honest lieutenant
+    packet's L holds the sender's tuple gathered in the ORDER IN WHICH THAT
+    SENDER RECEIVED P (the wire order of the packet that delivered P).
+
+    The logs predate the current tfg.py (they print 'w =' where tfg.py:136
+    prints '|W| ='); in that version the tuple follows the received order,
+    while the current code iterates the rebuilt set (tfg.py:240, 291).  Either
+    way the gather kernel must reproduce a tuple from a given index order."""
+    logs = json.loads((GOLDEN / "logs.json").read_text())
+    arrays = np.load(GOLDEN / "logs.npz")
+    checked = 0
+    for info in logs:
+        L = arrays[info["file"][:-4]]
+        pk = info["packets"]
+        for i, p in enumerate(pk):
+            if p["src"] < 2 or p["bad"] or not p["P_order"]:
+                continue
+            li = engine.to_device(L[p["src"]])
+            incoming = [q for q in pk[:i] if q["dst"] == p["src"] and set(q["P_order"]) == set(p["P_order"])]
+            hits = [[int(x) for x in engine.gather(li, np.array(q["P_order"], np.int64))] in p["L"]
+                    for q in incoming]
+            assert any(hits), (info["file"], p["src"], p["dst"])
+            checked += 1
+    assert checked == 205

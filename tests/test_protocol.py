@@ -1,0 +1,73 @@
+"""Protocol parity: the host (exact mode) against the reference's own QBA runs.
+
+tests/golden/protocol.json holds, for 60 injected-list cases, what the
+reference tfg.py produced on the same in-process MPI world with the same
+per-rank seeds: decisions, dishonest ids, Success, every honest lieutenant's
+V_i, per-rank consistent() accept/reject counts, packets sent and the total
+message count / bytes on the wire.  The host must reproduce all of it.
+
+The CPU variant drives the host with a numpy oracle engine (host logic only);
+the GPU variant runs the product path through libqba's HIP kernels.
+"""
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, sub
+from oracle_engine import OracleEngine
+
+CASES = json.loads((GOLDEN / "protocol.json").read_text())
+LISTS = np.load(GOLDEN / "protocol_lists.npz")
+
+
+def _compare(run, want):
+    assert run.error == want["error"]
+    assert run.error_ranks == want["error_ranks"]
+    assert run.result["decisions"] == want["decisions"]
+    assert run.result["dishonest"] == want["dishonest"]
+    assert run.result["success"] == want["success"]
+    assert {str(k): v for k, v in run.V.items()} == want["V"]
+    assert run.accept == want["accept"]
+    assert run.reject == want["reject"]
+    assert run.sent == want["sent"]
+    assert run.messages == want["messages"]
+    assert run.bytes == want["bytes"]
+
+
+def _run(engine, case):
+    protocol = sub("protocol")
+    return protocol.run_local(case["n"], case["sizeL"], case["nDishonest"], engine,
+                              seed=case["seed"], lists=LISTS[case["name"]], timeout=60)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_protocol_exact_cpu_host(case):
+    _compare(_run(OracleEngine(), case), case["exact"])
+
+
+@pytest.mark.gpu
+def test_protocol_exact_gpu(engine):
+    for case in CASES:
+        _compare(_run(engine, case), case["exact"])
+
+
+def test_consistent_host_kat():
+    """Host consistent(): Cond1 / StopIteration semantics with the oracle engine."""
+    protocol = sub("protocol")
+    eng = OracleEngine()
+    for case in json.loads((GOLDEN / "consistent.json").read_text()):
+        L = {tuple(t) for t in case["L"]}
+        if "error" in case:
+            with pytest.raises(StopIteration):
+                protocol.consistent(case["v"], L, case["w"], eng)
+        else:
+            assert protocol.consistent(case["v"], L, case["w"], eng) == case["result"]
+
+
+def test_decide_order_empty_raises():
+    protocol = sub("protocol")
+    with pytest.raises(ValueError):
+        protocol.decide_order(set(), 3, False)
+    assert protocol.decide_order({4, 2}, 9, False) == 2
+    assert protocol.decide_order(set(), 9, True) == 9

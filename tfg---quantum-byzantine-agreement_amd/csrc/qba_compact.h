@@ -1,0 +1,103 @@
+// qba_compact.h -- order-preserving stream compaction (count / scan / emit).
+//
+// Used where the reference builds an ordered selection: the ascending
+// isQCorrList (tfg.py:327), the P filter that keeps isQCorr's iteration order
+// (tfg.py:182) and the support of a statevector (resource compilation).
+// Three launches: per-tile counts, a single-workgroup exclusive scan of the
+// tile counts, and an emit pass that re-evaluates the predicate and writes
+// each selected item at its global rank.  A tile is 256 threads x 16 items;
+// each thread owns 16 consecutive items.
+#pragma once
+
+#include "qba_internal.h"
+
+#define QBA_CT_THREADS 256
+#define QBA_CT_ITEMS 16
+#define QBA_CT_TILE (QBA_CT_THREADS * QBA_CT_ITEMS)
+
+template <class Pred>
+__global__ void __launch_bounds__(QBA_CT_THREADS)
+    qba_k_compact_count(Pred p, int64_t n, int32_t *__restrict__ tile_counts) {
+  __shared__ int32_t wsum[QBA_CT_THREADS / 64];
+  const int64_t tile = blockIdx.x;
+  const int64_t base = tile * QBA_CT_TILE + (int64_t)threadIdx.x * QBA_CT_ITEMS;
+  int32_t c = 0;
+  for (int k = 0; k < QBA_CT_ITEMS; ++k) {
+    const int64_t i = base + k;
+    if (i < n && p.test(i)) ++c;
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t s = 0;
+    for (int w = 0; w < QBA_CT_THREADS / 64; ++w) s += wsum[w];
+    tile_counts[tile] = s;
+  }
+}
+
+// exclusive scan of ntiles int32 counts -> int64 offsets, total in *total
+__global__ void __launch_bounds__(1024)
+    qba_k_compact_scan(const int32_t *__restrict__ counts, int64_t ntiles,
+                       int64_t *__restrict__ offsets, int64_t *__restrict__ total);
+
+template <class Pred>
+__global__ void __launch_bounds__(QBA_CT_THREADS)
+    qba_k_compact_emit(Pred p, int64_t n, const int64_t *__restrict__ offsets, int64_t cap) {
+  __shared__ int32_t wsum[QBA_CT_THREADS / 64];
+  const int64_t tile = blockIdx.x;
+  const int64_t base = tile * QBA_CT_TILE + (int64_t)threadIdx.x * QBA_CT_ITEMS;
+  uint32_t bits = 0;
+  for (int k = 0; k < QBA_CT_ITEMS; ++k) {
+    const int64_t i = base + k;
+    if (i < n && p.test(i)) bits |= 1u << k;
+  }
+  const int32_t c = __popc(bits);
+  // inclusive scan over the wave
+  int32_t incl = c;
+  const int lane = threadIdx.x & 63;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wsum[threadIdx.x >> 6] = incl;
+  __syncthreads();
+  int32_t wbase = 0;
+  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) wbase += wsum[w];
+  int64_t pos = offsets[tile] + wbase + incl - c;
+  while (bits) {
+    const int k = __ffs(bits) - 1;
+    bits &= bits - 1;
+    if (pos < cap) p.emit(base + k, pos);
+    ++pos;
+  }
+}
+
+// Runs the three passes on `stream`, then waits and returns the total in *count_host.
+template <class Pred>
+static int qba_compact(qba_ctx *ctx, Pred p, int64_t n, int64_t cap, int64_t *count_host,
+                       hipStream_t stream) {
+  if (n <= 0) {
+    *count_host = 0;
+    return QBA_OK;
+  }
+  const int64_t ntiles = (n + QBA_CT_TILE - 1) / QBA_CT_TILE;
+  const size_t need = ntiles * sizeof(int32_t) + ntiles * sizeof(int64_t) + 64;
+  int rc = qba_ensure_scan(ctx, need);
+  if (rc) return rc;
+  int64_t *offsets = reinterpret_cast<int64_t *>(ctx->scan);
+  int32_t *counts = reinterpret_cast<int32_t *>(offsets + ntiles);
+  if (ntiles > 0x7fffffffLL) return qba_fail(QBA_EUNSUPPORTED, "compaction: input too large");
+  hipLaunchKernelGGL(qba_k_compact_count<Pred>, dim3((unsigned)ntiles), dim3(QBA_CT_THREADS), 0,
+                     stream, p, n, counts);
+  QBA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(qba_k_compact_scan, dim3(1), dim3(1024), 0, stream, counts, ntiles, offsets,
+                     ctx->count1);
+  QBA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(qba_k_compact_emit<Pred>, dim3((unsigned)ntiles), dim3(QBA_CT_THREADS), 0,
+                     stream, p, n, offsets, cap);
+  QBA_HIP(hipGetLastError());
+  QBA_HIP(hipMemcpyAsync(count_host, ctx->count1, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+  QBA_HIP(hipStreamSynchronize(stream));
+  return QBA_OK;
+}

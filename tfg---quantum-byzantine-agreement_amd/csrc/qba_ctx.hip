@@ -1,0 +1,96 @@
+// qba_ctx.hip -- library context, error channel and scratch management.
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <string>
+
+#include "qba_internal.h"
+
+static thread_local std::string g_last_error;
+
+int qba_fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+extern "C" const char *qba_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int qba_version(void) { return 100; /* 0.1.0 */ }
+
+int qba_set_device(qba_ctx *ctx) {
+  int cur = -1;
+  QBA_HIP(hipGetDevice(&cur));
+  if (cur != ctx->device) QBA_HIP(hipSetDevice(ctx->device));
+  return QBA_OK;
+}
+
+extern "C" int qba_init(int device, qba_ctx **out) {
+  if (!out) return qba_fail(QBA_EINVAL, "qba_init: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0)
+    return qba_fail(QBA_EHIP, "qba_init: no HIP device visible (" +
+                                  std::string(hipGetErrorString(e)) + ")");
+  if (device < 0 || device >= ndev)
+    return qba_fail(QBA_EINVAL, "qba_init: device " + std::to_string(device) + " out of range");
+  QBA_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  QBA_HIP(hipGetDeviceProperties(&prop, device));
+  std::string arch = prop.gcnArchName;
+  if (arch.rfind("gfx950", 0) != 0)
+    return qba_fail(QBA_EUNSUPPORTED, "qba_init: built for gfx950 (MI355X), found " + arch);
+  qba_ctx *ctx = new qba_ctx();
+  ctx->device = device;
+  ctx->num_cus = prop.multiProcessorCount;
+  if (hipMalloc(&ctx->flag, 64) != hipSuccess || hipMalloc(&ctx->count1, 64) != hipSuccess ||
+      hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess) {
+    delete ctx;
+    return qba_fail(QBA_ENOMEM, "qba_init: hipMalloc of flags failed");
+  }
+  *out = ctx;
+  return QBA_OK;
+}
+
+extern "C" int qba_destroy(qba_ctx *ctx) {
+  if (!ctx) return QBA_OK;
+  (void)hipSetDevice(ctx->device);
+  for (int n = 0; n <= QBA_MAX_PARTIES; ++n) {
+    if (ctx->prog_dev[n]) (void)hipFree(ctx->prog_dev[n]);
+    free(ctx->prog_host[n]);
+  }
+  if (ctx->slab) (void)hipFree(ctx->slab);
+  if (ctx->scan) (void)hipFree(ctx->scan);
+  if (ctx->flag) (void)hipFree(ctx->flag);
+  if (ctx->count1) (void)hipFree(ctx->count1);
+  if (ctx->stats) (void)hipFree(ctx->stats);
+  delete ctx;
+  return QBA_OK;
+}
+
+static int ensure(void *&ptr, size_t &have, size_t want, const char *what) {
+  if (have >= want) return QBA_OK;
+  if (ptr) {
+    QBA_HIP(hipDeviceSynchronize());
+    QBA_HIP(hipFree(ptr));
+    ptr = nullptr;
+    have = 0;
+  }
+  size_t sz = want + want / 4 + 4096;
+  if (hipMalloc(&ptr, sz) != hipSuccess)
+    return qba_fail(QBA_ENOMEM, std::string("scratch allocation failed: ") + what);
+  have = sz;
+  return QBA_OK;
+}
+
+int qba_ensure_slab(qba_ctx *ctx, size_t bytes) { return ensure(ctx->slab, ctx->slab_bytes, bytes, "slab"); }
+int qba_ensure_scan(qba_ctx *ctx, size_t bytes) { return ensure(ctx->scan, ctx->scan_bytes, bytes, "scan"); }
+
+extern "C" int qba_last_stats(qba_ctx *ctx, int64_t *out2) {
+  if (!ctx || !out2) return qba_fail(QBA_EINVAL, "qba_last_stats: bad arguments");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  QBA_HIP(hipDeviceSynchronize());
+  QBA_HIP(hipMemcpy(out2, ctx->stats, 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+  return QBA_OK;
+}

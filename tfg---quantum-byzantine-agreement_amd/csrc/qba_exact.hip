@@ -1,0 +1,194 @@
+// qba_exact.hip -- exact-order checks for bit-exact protocol parity, and the
+// wire-compatible bit codec.
+//
+// The reference builds every party's tuple in its own set-iteration order
+// (tfg.py:189, 291) and compares tuples position by position (tfg.py:97-98),
+// so parity with it needs the host's index orders, not a canonical one.  The
+// host keeps the Python sets; these kernels do the per-element work.
+#include "qba_compact.h"
+
+__global__ void __launch_bounds__(1024)
+    qba_k_compact_scan(const int32_t *__restrict__ counts, int64_t ntiles,
+                       int64_t *__restrict__ offsets, int64_t *__restrict__ total) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (ntiles + 1023) / 1024;
+  const int64_t lo = t * per, hi = lo + per < ntiles ? lo + per : ntiles;
+  int64_t s = 0;
+  for (int64_t i = lo; i < hi; ++i) s += counts[i];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    const int64_t y = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += y;
+    __syncthreads();
+  }
+  int64_t run = part[t] - s;
+  for (int64_t i = lo; i < hi; ++i) {
+    offsets[i] = run;
+    run += counts[i];
+  }
+  if (t == 1023) *total = part[1023];
+}
+
+// --- isQCorrList = {k : Li[k] != Lc[k]}  (tfg.py:327) -------------------------------
+struct QbaIsqPred {
+  const uint8_t *l0, *l1;
+  int64_t *out;
+  __device__ bool test(int64_t i) const { return l0[i] != l1[i]; }
+  __device__ void emit(int64_t i, int64_t pos) const { out[pos] = i; }
+};
+
+extern "C" int qba_isq_indices(qba_ctx *ctx, const uint8_t *li, const uint8_t *lc, uint64_t count,
+                               int64_t *idx, int64_t cap, int64_t *count_host, qba_stream stream) {
+  if (!ctx || !count_host || (count && (!li || !lc)) || (cap > 0 && !idx) || cap < 0)
+    return qba_fail(QBA_EINVAL, "qba_isq_indices: bad arguments");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  return qba_compact(ctx, QbaIsqPred{li, lc, idx}, (int64_t)count, cap, count_host,
+                     (hipStream_t)stream);
+}
+
+// --- P = {x in isQCorr : Lc[x] == v}, isQCorr's iteration order kept (tfg.py:182) ------
+struct QbaSelPred {
+  const int64_t *order;
+  const uint8_t *lc;
+  int64_t v;
+  int64_t *out;
+  __device__ bool test(int64_t i) const { return (int64_t)lc[order[i]] == v; }
+  __device__ void emit(int64_t i, int64_t pos) const { out[pos] = order[i]; }
+};
+
+extern "C" int qba_select_eq(qba_ctx *ctx, const int64_t *order, int64_t m, const uint8_t *lc,
+                             int64_t v, int64_t *out, int64_t *count_host, qba_stream stream) {
+  if (!ctx || !count_host || m < 0 || (m && (!order || !lc || !out)))
+    return qba_fail(QBA_EINVAL, "qba_select_eq: bad arguments");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  return qba_compact(ctx, QbaSelPred{order, lc, v, out}, m, m, count_host, (hipStream_t)stream);
+}
+
+// --- tuple(Li[j] for j in P)  (tfg.py:189, 291) --------------------------------------
+__global__ void qba_k_gather(const uint8_t *__restrict__ li, const int64_t *__restrict__ idx,
+                             int64_t m, int64_t *__restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = li[idx[i]];
+}
+
+// Indices must lie in [0, list_len): verified on the device first so a bad
+// packet cannot make the gather read out of bounds.
+__global__ void qba_k_bounds(const int64_t *__restrict__ idx, int64_t m, int64_t len,
+                             int32_t *__restrict__ bad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (idx[i] < 0 || idx[i] >= len) atomicOr(bad, 1);
+}
+
+extern "C" int qba_gather(qba_ctx *ctx, const uint8_t *li, uint64_t list_len, const int64_t *idx,
+                          int64_t m, int64_t *out, qba_stream stream) {
+  if (!ctx || m < 0 || (m && (!li || !idx || !out)))
+    return qba_fail(QBA_EINVAL, "qba_gather: bad arguments");
+  if (m == 0) return QBA_OK;
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned grid = (unsigned)std::min<int64_t>((m + 255) / 256, 4096);
+  QBA_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int32_t), s));
+  hipLaunchKernelGGL(qba_k_bounds, dim3(grid), dim3(256), 0, s, idx, m, (int64_t)list_len, ctx->flag);
+  int32_t bad = 0;
+  QBA_HIP(hipMemcpyAsync(&bad, ctx->flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  QBA_HIP(hipStreamSynchronize(s));
+  if (bad) return qba_fail(QBA_EINVAL, "qba_gather: index outside the list");
+  hipLaunchKernelGGL(qba_k_gather, dim3(grid), dim3(256), 0, s, li, idx, m, out);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}
+
+// --- consistent(v, L, w): Cond2 and Cond3 (tfg.py:93-98) ---------------------------
+// One thread per position k: every value must satisfy 0 <= x <= w and x != v
+// (inclusive w, as the reference), and the m values at k must be pairwise
+// distinct.  Any violation clears the flag.
+__global__ void qba_k_consistent(const int64_t *__restrict__ t, int64_t m, int64_t len, int64_t v,
+                                 int64_t w, int32_t *__restrict__ ok) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < len;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    bool good = true;
+    for (int64_t a = 0; a < m && good; ++a) {
+      const int64_t x = t[a * len + k];
+      if (x < 0 || x > w || x == v) good = false;
+      for (int64_t b = a + 1; b < m && good; ++b)
+        if (t[b * len + k] == x) good = false;
+    }
+    if (!good) atomicAnd(ok, 0);
+  }
+}
+
+extern "C" int qba_consistent(qba_ctx *ctx, const int64_t *tuples, int64_t m, int64_t len,
+                              int64_t v, int64_t w, int32_t *ok_host, qba_stream stream) {
+  if (!ctx || !ok_host || m < 1 || len < 0 || (len && !tuples))
+    return qba_fail(QBA_EINVAL, "qba_consistent: bad arguments (m >= 1 required)");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int32_t one = 1;
+  QBA_HIP(hipMemcpyAsync(ctx->flag, &one, sizeof(int32_t), hipMemcpyHostToDevice, s));
+  if (len > 0) {
+    const unsigned grid = (unsigned)std::min<int64_t>((len + 255) / 256, 4096);
+    hipLaunchKernelGGL(qba_k_consistent, dim3(grid), dim3(256), 0, s, tuples, m, len, v, w, ctx->flag);
+    QBA_HIP(hipGetLastError());
+  }
+  QBA_HIP(hipMemcpyAsync(ok_host, ctx->flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  QBA_HIP(hipStreamSynchronize(s));
+  return QBA_OK;
+}
+
+// --- wire codec: rawS bits (one int64 per measured bit, MSB first) <-> values ---------
+__global__ void qba_k_bits_to_values(const int64_t *__restrict__ raw, uint64_t count, int nq,
+                                     uint8_t *__restrict__ vals) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < count;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t v = 0;
+    for (int j = 0; j < nq; ++j) v = (v << 1) | (uint32_t)(raw[k * nq + j] & 1);
+    vals[k] = (uint8_t)v;
+  }
+}
+
+__global__ void qba_k_values_to_bits(const uint8_t *__restrict__ vals, uint64_t count, int nq,
+                                     int64_t *__restrict__ raw) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count * nq;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = i / nq;
+    const int j = (int)(i - k * nq);
+    raw[i] = (vals[k] >> (nq - 1 - j)) & 1;
+  }
+}
+
+extern "C" int qba_bits_to_values(qba_ctx *ctx, const int64_t *raw, uint64_t count, int nq,
+                                  uint8_t *vals, qba_stream stream) {
+  if (!ctx || nq < 1 || nq > 8 || (count && (!raw || !vals)))
+    return qba_fail(QBA_EINVAL, "qba_bits_to_values: bad arguments (1 <= nq <= 8)");
+  if (count == 0) return QBA_OK;
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  const unsigned grid = (unsigned)std::min<uint64_t>((count + 255) / 256, 8192);
+  hipLaunchKernelGGL(qba_k_bits_to_values, dim3(grid), dim3(256), 0, (hipStream_t)stream, raw,
+                     count, nq, vals);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}
+
+extern "C" int qba_values_to_bits(qba_ctx *ctx, const uint8_t *vals, uint64_t count, int nq,
+                                  int64_t *raw, qba_stream stream) {
+  if (!ctx || nq < 1 || nq > 8 || (count && (!raw || !vals)))
+    return qba_fail(QBA_EINVAL, "qba_values_to_bits: bad arguments (1 <= nq <= 8)");
+  if (count == 0) return QBA_OK;
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  const unsigned grid = (unsigned)std::min<uint64_t>((count * nq + 255) / 256, 8192);
+  hipLaunchKernelGGL(qba_k_values_to_bits, dim3(grid), dim3(256), 0, (hipStream_t)stream, vals,
+                     count, nq, raw);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}

@@ -1,0 +1,136 @@
+// qba_internal.h -- shared definitions of libqba (host + gfx950 device code).
+//
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11) is the counter-based
+// generator; the counter is the GLOBAL list-entry index, so a shard computes
+// exactly the entries it owns and lists are bit-identical at 1/2/4/8 GPUs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/qba.h"
+
+#define QBA_MAX_FACTORS 16
+#define QBA_MAX_TABLE 4096   // uint64 table entries per kind (LDS budget)
+#define QBA_BLOCK 256        // threads per workgroup for the list kernels
+#define QBA_EPT 4            // entries per thread per step: one dword per list row
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10
+// ---------------------------------------------------------------------------
+struct QbaU4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ __forceinline__ QbaU4 qba_philox(uint32_t c0, uint32_t c1, uint32_t c2,
+                                                     uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return QbaU4{c0, c1, c2, c3};
+}
+
+// ---------------------------------------------------------------------------
+// Compiled resource program (one per circuit kind), see qba_resource.cpp.
+//
+// Random-bit schedule of one entry e (identical in the CPU twin,
+// oracle/sampler_ref.c):
+//   block b = philox(ctr = {e_lo, e_hi, b, 0}, key = {seed_lo, seed_hi})
+//   block 0 = {x0, x1, x2, x3};  isQ = x0 & 1
+//   Q:    F = x2 | x3 << 32 drives the permutation; table words are
+//         x1, then block 1 words 0..3, block 2, ...
+//   notQ: table words are x1, x2, x3, then block 1 words 0..3, ...
+//   Permutation retry a = 1, 2, ...: F = y0 | y1 << 32 of block 0x80000000 + a.
+// Each factor takes `bits` column bits at (col_word, col_shift), and when it
+// is not uniform a 32-bit u from its own word u_word: outcome pattern
+// = (u < thr[col]) ? pat[col] : apat[col].
+// ---------------------------------------------------------------------------
+struct QbaFactor {
+  int32_t bits;
+  int32_t uniform;
+  int32_t offset;     // into the concatenated table of this program
+  int32_t col_word;
+  int32_t col_shift;
+  int32_t u_word;     // -1 when uniform
+};
+
+struct QbaProgram {
+  int32_t nfac;
+  int32_t table_len;
+  int32_t any_nonuniform;
+  int32_t valid;
+  uint64_t perm_t;  // 2^64 mod n!  (Lemire rejection threshold), Q program only
+  QbaFactor fac[QBA_MAX_FACTORS];
+};
+
+// Device image of the compiled programs for one n: [prog notq][prog q]
+// followed by pat[T], apat[T], thr[T] (uint64) where T = total table entries
+// (notq tables first).
+struct QbaProgramSet {
+  QbaProgram prog[2];
+  int32_t table_total;
+  int32_t any_nonuniform;
+  int32_t n;
+  int32_t pad;
+};
+
+// ---------------------------------------------------------------------------
+// error reporting / context
+// ---------------------------------------------------------------------------
+int qba_fail(int code, const std::string &msg);
+#define QBA_HIP(call)                                                                     \
+  do {                                                                                    \
+    hipError_t _e = (call);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      return qba_fail(QBA_EHIP, std::string(#call) + ": " + hipGetErrorString(_e));       \
+  } while (0)
+
+// host copy of one compiled program (tables before concatenation)
+struct QbaHostProgram {
+  QbaProgram p{};
+  std::vector<uint64_t> pat, apat, thr;
+};
+
+struct qba_ctx {
+  int device = 0;
+  int num_cus = 256;
+  // per-n compiled programs (device image + host copy)
+  void *prog_dev[QBA_MAX_PARTIES + 1] = {};
+  size_t prog_bytes[QBA_MAX_PARTIES + 1] = {};
+  void *prog_host[QBA_MAX_PARTIES + 1] = {};  // QbaProgramSet + tables, host copy
+  bool compiled[QBA_MAX_PARTIES + 1][2] = {};
+  QbaHostProgram hprog[QBA_MAX_PARTIES + 1][2];
+  // scratch
+  void *slab = nullptr;
+  size_t slab_bytes = 0;
+  void *scan = nullptr;  // compaction scratch
+  size_t scan_bytes = 0;
+  int32_t *flag = nullptr;  // 1-word device flag
+  int64_t *count1 = nullptr; // 1-word device counter
+  int64_t *stats = nullptr;  // [2]: last counts launch: Q entries with a value >= w, spare
+};
+
+int qba_ensure_slab(qba_ctx *ctx, size_t bytes);
+int qba_ensure_scan(qba_ctx *ctx, size_t bytes);
+int qba_set_device(qba_ctx *ctx);
+
+static inline int qba_nq(int n) {  // ceil(log2(n+1)), tfg.py:317
+  int q = 0;
+  while ((1 << q) < n + 1) ++q;
+  return q;
+}
+
+static inline int64_t qba_ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

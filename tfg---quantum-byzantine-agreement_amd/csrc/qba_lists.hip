@@ -1,0 +1,453 @@
+// qba_lists.hip -- the data-parallel hot path on gfx950:
+//   * Born sampling of list entries (tfg.py:68-84 + 128-129) from the compiled
+//     factored alias-table program, Philox4x32-10 keyed by the global entry;
+//   * the count-mode check pass (tfg.py:87-98, 182, 189, 291-294, 327):
+//     per Q-correlated entry, H[u][g][x] += 1 for every group g and
+//     C[u][g][h] += 1 for every equal pair, u = L1[k];
+//   * the fused sample+check kernel that writes each list byte once and
+//     counts from registers.
+//
+// Layout: lists[g][k] uint8, row stride ld (SoA: a party's list is one row).
+// A thread owns 4 consecutive entries (one dword per row), so every row store
+// / load of a wave is 256 contiguous bytes.  Histograms are privatised per
+// workgroup in LDS and flushed as u32 partials to a slab that a second
+// kernel reduces into int64 (bitwise reproducible, no global atomics).
+#include <type_traits>
+
+#include "qba_internal.h"
+
+template <int NP>
+struct QCfg {
+  static constexpr int G = NP + 1;  // measured groups (n parties + the commander's extra)
+  static constexpr int NQ = (G <= 2) ? 1 : (G <= 4) ? 2 : (G <= 8) ? 3 : 4;
+  static constexpr int N = G * NQ;  // qubits of the circuit (tfg.py:44)
+  static constexpr int W = 1 << NQ;  // |W| (tfg.py:318)
+  static constexpr int HB = W * G * W;
+  static constexpr int CB = W * G * G;
+  static constexpr int STATS = 2;  // [0] Q entries with a value >= W (invalid), [1] spare
+  static constexpr int NBINS = HB + CB + STATS;
+  using Out = typename std::conditional<(N <= 32), uint32_t, uint64_t>::type;
+  static constexpr Out M = (Out)(W - 1);
+  __host__ __device__ static constexpr int shift(int g) { return N - (g + 1) * NQ; }
+  __host__ __device__ static constexpr Out identity() {
+    Out p = 0;
+    for (int g = 1; g <= NP; ++g) p |= (Out)g << shift(g);
+    return p;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// random words of one entry (schedule documented in qba_internal.h)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t qba_word(int kind, int k, const QbaU4 &x, uint32_t elo,
+                                             uint32_t ehi, uint32_t k0, uint32_t k1) {
+  const int base = kind ? 1 : 3;
+  if (k < base) return k == 0 ? x.y : (k == 1 ? x.z : x.w);
+  const int kk = k - base;
+  const QbaU4 y = qba_philox(elo, ehi, 1u + (uint32_t)(kk >> 2), 0u, k0, k1);
+  const int s = kk & 3;
+  return s == 0 ? y.x : (s == 1 ? y.y : (s == 2 ? y.z : y.w));
+}
+
+template <typename Out>
+__device__ __forceinline__ Out qba_draw(const QbaProgram &P, int kind, const QbaU4 &x,
+                                        uint32_t elo, uint32_t ehi, uint32_t k0, uint32_t k1,
+                                        const uint64_t *pat, const uint64_t *apat,
+                                        const uint64_t *thr) {
+  Out out = 0;
+  const int nf = P.nfac;
+  for (int f = 0; f < nf; ++f) {
+    const QbaFactor F = P.fac[f];
+    const uint32_t wv = qba_word(kind, F.col_word, x, elo, ehi, k0, k1);
+    const uint32_t col = (wv >> F.col_shift) & ((1u << F.bits) - 1u);
+    uint64_t p = pat[F.offset + col];
+    if (!F.uniform) {
+      const uint32_t u = qba_word(kind, F.u_word, x, elo, ehi, k0, k1);
+      if ((uint64_t)u >= thr[F.offset + col]) p = apat[F.offset + col];
+    }
+    out ^= (Out)p;
+  }
+  return out;
+}
+
+// Uniform permutation pi of 1..n in the outcome layout (field g = pi(g)):
+// mixed-radix digits of floor(F * n! / 2^64) drive Fisher-Yates; Lemire's
+// test on the final fraction makes it exactly uniform.
+template <int NP>
+__device__ __forceinline__ bool qba_perm(uint64_t F, uint64_t t, typename QCfg<NP>::Out &mask) {
+  using C = QCfg<NP>;
+  using Out = typename C::Out;
+  Out P = C::identity();
+#pragma unroll
+  for (int i = NP; i >= 2; --i) {
+    const uint64_t lo = (F & 0xffffffffull) * (uint64_t)i;
+    const uint64_t hi = (F >> 32) * (uint64_t)i + (lo >> 32);
+    const uint32_t d = (uint32_t)(hi >> 32);
+    F = (hi << 32) | (lo & 0xffffffffull);
+    const int si = C::shift(i);
+    const int sj = C::N - (int)(d + 2) * C::NQ;  // field j = 1 + d
+    const Out a = (P >> si) & C::M;
+    const Out b = (P >> sj) & C::M;
+    const Out tt = a ^ b;
+    P ^= (tt << si) | (tt << sj);
+  }
+  mask = P;
+  return F >= t;
+}
+
+template <int NP>
+__device__ __forceinline__ typename QCfg<NP>::Out qba_sample_entry(
+    uint64_t e, uint32_t k0, uint32_t k1, const QbaProgramSet *__restrict__ ps,
+    const uint64_t *pat, const uint64_t *apat, const uint64_t *thr) {
+  using Out = typename QCfg<NP>::Out;
+  const uint32_t elo = (uint32_t)e, ehi = (uint32_t)(e >> 32);
+  const QbaU4 x = qba_philox(elo, ehi, 0u, 0u, k0, k1);
+  Out out;
+  if (x.x & 1u) {  // Q-correlated shot (tfg.py:69, 74)
+    const uint64_t t = ps->prog[1].perm_t;
+    Out mask;
+    bool ok = qba_perm<NP>((uint64_t)x.z | ((uint64_t)x.w << 32), t, mask);
+    for (uint32_t a = 1; !ok; ++a) {  // probability ~ n!/2^64 per entry
+      const QbaU4 y = qba_philox(elo, ehi, 0x80000000u + a, 0u, k0, k1);
+      ok = qba_perm<NP>((uint64_t)y.x | ((uint64_t)y.y << 32), t, mask);
+    }
+    out = qba_draw<Out>(ps->prog[1], 1, x, elo, ehi, k0, k1, pat, apat, thr) ^ mask;
+  } else {  // not-Q-correlated shot (tfg.py:72)
+    out = qba_draw<Out>(ps->prog[0], 0, x, elo, ehi, k0, k1, pat, apat, thr);
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// count one entry (values are byte j of row[g])
+// ---------------------------------------------------------------------------
+template <int NP>
+__device__ __forceinline__ void qba_count_entry(const uint32_t (&row)[NP + 1], int j,
+                                                uint32_t *hist) {
+  using C = QCfg<NP>;
+  uint32_t l[C::G];
+  uint32_t any = 0;
+#pragma unroll
+  for (int g = 0; g < C::G; ++g) {
+    l[g] = (row[g] >> (8 * j)) & 0xffu;
+    any |= l[g];
+  }
+  if (l[0] == l[1]) return;  // not Q-correlated (tfg.py:327)
+  if (any >= (uint32_t)C::W) {
+    atomicAdd(&hist[C::HB + C::CB + 0], 1u);
+    return;
+  }
+  uint32_t *h = hist + l[1] * (C::G * C::W);
+  uint32_t seen = 0;
+#pragma unroll
+  for (int g = 0; g < C::G; ++g) {
+    atomicAdd(&h[g * C::W + l[g]], 1u);
+    seen |= 1u << l[g];
+  }
+  if (__popc(seen) != C::G) {  // some pair collides: exact slow path
+    uint32_t *c = hist + C::HB + l[1] * (C::G * C::G);
+#pragma unroll
+    for (int g = 0; g < C::G; ++g)
+#pragma unroll
+      for (int k = g + 1; k < C::G; ++k)
+        if (l[g] == l[k]) atomicAdd(&c[g * C::G + k], 1u);
+  }
+}
+
+// MODE 0: sample -> lists;  MODE 1: sample -> lists + counts;  MODE 2: lists -> counts
+template <int NP, int MODE>
+__global__ void __launch_bounds__(QBA_BLOCK)
+    qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
+                uint64_t count, uint8_t *__restrict__ lists, uint64_t ld,
+                uint32_t *__restrict__ slab) {
+  using C = QCfg<NP>;
+  using Out = typename C::Out;
+  extern __shared__ __align__(16) uint64_t lds[];
+  const int tid = threadIdx.x;
+  const uint64_t *pat = lds, *apat = lds, *thr = lds;
+  uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
+  if constexpr (MODE != 2) {
+    const int T = ps->table_total;
+    const uint64_t *tab = reinterpret_cast<const uint64_t *>(ps + 1);
+    const int ntab = ps->any_nonuniform ? 3 * T : T;
+    for (int i = tid; i < ntab; i += QBA_BLOCK) lds[i] = tab[i];
+    apat = lds + T;
+    thr = lds + 2 * T;
+    hist = reinterpret_cast<uint32_t *>(lds + ntab);
+  }
+  if (MODE != 0)
+    for (int i = tid; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
+  __syncthreads();
+
+  const uint64_t nquad = (count + 3) >> 2;
+  for (uint64_t q = (uint64_t)blockIdx.x * QBA_BLOCK + tid; q < nquad;
+       q += (uint64_t)gridDim.x * QBA_BLOCK) {
+    const uint64_t c0 = q << 2;
+    const int valid = (count - c0) >= 4 ? 4 : (int)(count - c0);
+    uint32_t row[C::G];
+    if constexpr (MODE == 2) {
+      if (valid == 4) {
+#pragma unroll
+        for (int g = 0; g < C::G; ++g)
+          row[g] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(lists + g * ld + c0));
+      } else {
+#pragma unroll
+        for (int g = 0; g < C::G; ++g) {
+          row[g] = 0;
+          for (int j = 0; j < valid; ++j) row[g] |= (uint32_t)lists[g * ld + c0 + j] << (8 * j);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < C::G; ++g) row[g] = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < valid) {
+          const Out o = qba_sample_entry<NP>(first + c0 + j, k0, k1, ps, pat, apat, thr);
+#pragma unroll
+          for (int g = 0; g < C::G; ++g)
+            row[g] |= ((uint32_t)(o >> C::shift(g)) & (uint32_t)C::M) << (8 * j);
+        }
+      }
+      if (valid == 4) {
+#pragma unroll
+        for (int g = 0; g < C::G; ++g)
+          *reinterpret_cast<uint32_t *>(lists + g * ld + c0) = row[g];
+      } else {
+#pragma unroll
+        for (int g = 0; g < C::G; ++g)
+          for (int j = 0; j < valid; ++j) lists[g * ld + c0 + j] = (uint8_t)(row[g] >> (8 * j));
+      }
+    }
+    if (MODE != 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < valid) qba_count_entry<NP>(row, j, hist);
+    }
+  }
+  if (MODE != 0) {
+    __syncthreads();
+    uint32_t *dst = slab + (size_t)blockIdx.x * C::NBINS;
+    for (int i = tid; i < C::NBINS; i += QBA_BLOCK) dst[i] = hist[i];
+  }
+}
+
+// Sum the per-workgroup partials into the int64 outputs (see qba.h for shapes).
+template <int NP>
+__global__ void __launch_bounds__(256)
+    qba_k_reduce(const uint32_t *__restrict__ slab, int nblocks, int64_t *__restrict__ H,
+                 int64_t *__restrict__ Cc, int64_t *__restrict__ P, int64_t *__restrict__ stats,
+                 int accumulate) {
+  using C = QCfg<NP>;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  auto colsum = [&](int bin) {
+    int64_t s = 0;
+    for (int b = 0; b < nblocks; ++b) s += slab[(size_t)b * C::NBINS + bin];
+    return s;
+  };
+  auto put = [&](int64_t *dst, int64_t v) { *dst = accumulate ? *dst + v : v; };
+  if (i < C::HB) {
+    put(&H[i], colsum(i));
+    return;
+  }
+  int r = i - C::HB;
+  if (r < C::CB) {
+    const int u = r / (C::G * C::G), g = (r / C::G) % C::G, h = r % C::G;
+    if (g < h) {
+      const int64_t s = colsum(C::HB + r);
+      put(&Cc[r], s);
+      put(&Cc[(u * C::G + h) * C::G + g], s);
+    } else if (g == h) {
+      put(&Cc[r], colsum((u * C::G + 1) * C::W + u));  // |P_u| = H[u][1][u]
+    }
+    return;
+  }
+  r -= C::CB;
+  if (r < C::W) {
+    put(&P[r], colsum((r * C::G + 1) * C::W + r));
+    return;
+  }
+  r -= C::W;
+  if (r < C::STATS && stats) stats[r] = colsum(C::HB + C::CB + r);
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+struct QbaLaunch {
+  int n;
+  int mode;
+  const QbaProgramSet *ps;
+  uint64_t seed, first, count;
+  uint8_t *lists;
+  uint64_t ld;
+  int64_t *H, *C, *P, *stats;
+  int accumulate;
+  hipStream_t stream;
+};
+
+static int nbins_of(int n) {
+  const int g = n + 1, q = qba_nq(n), w = 1 << q;
+  return w * g * w + w * g * g + 2;
+}
+
+static int grid_for(qba_ctx *ctx, int mode, uint64_t count) {
+  const uint64_t nquad = (count + 3) >> 2;
+  const uint64_t per_block = (uint64_t)QBA_BLOCK * (mode == 0 ? 1 : 4);
+  uint64_t g = (nquad + per_block - 1) / per_block;
+  const uint64_t cap = (uint64_t)ctx->num_cus * (mode == 0 ? 8 : 4);
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  // keep every per-block u32 partial far from overflow
+  const uint64_t min_g = count / (1ull << 30) + 1;
+  if (g < min_g) g = min_g;
+  return (int)g;
+}
+
+template <int NP>
+static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
+  using C = QCfg<NP>;
+  const int grid = grid_for(ctx, L.mode, L.count);
+  size_t lds = 0;
+  if (L.mode != 2) {
+    const QbaProgramSet *hs = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP]);
+    lds += (size_t)(hs->any_nonuniform ? 3 : 1) * hs->table_total * sizeof(uint64_t);
+  }
+  if (L.mode != 0) lds += (size_t)C::NBINS * sizeof(uint32_t);
+  lds = (lds + 15) & ~(size_t)15;
+  if (lds == 0) lds = 16;
+  uint32_t *slab = nullptr;
+  if (L.mode != 0) {
+    int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBINS * sizeof(uint32_t));
+    if (rc) return rc;
+    slab = reinterpret_cast<uint32_t *>(ctx->slab);
+  }
+  const uint32_t k0 = (uint32_t)L.seed, k1 = (uint32_t)(L.seed >> 32);
+  auto go = [&](auto kern) -> int {
+    if (lds > 65536) QBA_HIP(hipFuncSetAttribute((const void *)kern,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(QBA_BLOCK), lds, L.stream, L.ps, k0, k1, L.first,
+                       L.count, L.lists, L.ld, slab);
+    QBA_HIP(hipGetLastError());
+    return QBA_OK;
+  };
+  int rc = L.mode == 0 ? go(qba_k_lists<NP, 0>) : L.mode == 1 ? go(qba_k_lists<NP, 1>)
+                                                             : go(qba_k_lists<NP, 2>);
+  if (rc || L.mode == 0) return rc;
+  const int items = C::HB + C::CB + C::W + C::STATS;
+  hipLaunchKernelGGL(qba_k_reduce<NP>, dim3((items + 255) / 256), dim3(256), 0, L.stream, slab,
+                     grid, L.H, L.C, L.P, L.stats, L.accumulate);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}
+
+static int dispatch(qba_ctx *ctx, const QbaLaunch &L) {
+  switch (L.n) {
+#define QBA_CASE(k) \
+  case k:           \
+    return launch_np<k>(ctx, L);
+    QBA_CASE(1) QBA_CASE(2) QBA_CASE(3) QBA_CASE(4) QBA_CASE(5) QBA_CASE(6) QBA_CASE(7)
+    QBA_CASE(8) QBA_CASE(9) QBA_CASE(10) QBA_CASE(11) QBA_CASE(12) QBA_CASE(13) QBA_CASE(14)
+    QBA_CASE(15)
+#undef QBA_CASE
+    default:
+      return qba_fail(QBA_EUNSUPPORTED, "n_parties must be in [1, 15]");
+  }
+}
+
+static int check_common(qba_ctx *ctx, int n, const uint8_t *lists, uint64_t count, uint64_t ld,
+                        const char *who) {
+  if (!ctx) return qba_fail(QBA_EINVAL, std::string(who) + ": ctx is NULL");
+  if (n < 1 || n > QBA_MAX_PARTIES)
+    return qba_fail(QBA_EUNSUPPORTED, std::string(who) + ": n_parties must be in [1, 15]");
+  if (count == 0) return QBA_OK;
+  if (!lists) return qba_fail(QBA_EINVAL, std::string(who) + ": lists is NULL");
+  if (ld < count || (ld & 3) || (reinterpret_cast<uintptr_t>(lists) & 3))
+    return qba_fail(QBA_EINVAL, std::string(who) +
+                                    ": need ld >= count, ld % 4 == 0 and a 4-byte aligned base");
+  return qba_set_device(ctx);
+}
+
+static int need_program(qba_ctx *ctx, int n, const char *who) {
+  if (!ctx->compiled[n][0] || !ctx->compiled[n][1])
+    return qba_fail(QBA_ESTATE, std::string(who) + ": no resource program compiled for n=" +
+                                    std::to_string(n) + " (call qba_resource_compile for both kinds)");
+  return QBA_OK;
+}
+
+static int zero_counts(int n, int64_t *H, int64_t *C, int64_t *P, hipStream_t s) {
+  const int g = n + 1, w = 1 << qba_nq(n);
+  QBA_HIP(hipMemsetAsync(H, 0, sizeof(int64_t) * w * g * w, s));
+  QBA_HIP(hipMemsetAsync(C, 0, sizeof(int64_t) * w * g * g, s));
+  QBA_HIP(hipMemsetAsync(P, 0, sizeof(int64_t) * w, s));
+  return QBA_OK;
+}
+
+extern "C" int qba_sample(qba_ctx *ctx, int n, uint64_t seed, uint64_t first, uint64_t count,
+                          uint8_t *lists, uint64_t ld, qba_stream stream) {
+  int rc = check_common(ctx, n, lists, count, ld, "qba_sample");
+  if (rc || count == 0) return rc;
+  if ((rc = need_program(ctx, n, "qba_sample"))) return rc;
+  QbaLaunch L{n, 0, (const QbaProgramSet *)ctx->prog_dev[n], seed, first, count, lists, ld,
+              nullptr, nullptr, nullptr, nullptr, 0, (hipStream_t)stream};
+  return dispatch(ctx, L);
+}
+
+extern "C" int qba_sample_check(qba_ctx *ctx, int n, uint64_t seed, uint64_t first,
+                                uint64_t count, uint8_t *lists, uint64_t ld, int64_t *H,
+                                int64_t *C, int64_t *P, int accumulate, qba_stream stream) {
+  int rc = check_common(ctx, n, lists, count, ld, "qba_sample_check");
+  if (rc) return rc;
+  if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_sample_check: H, C and P are required");
+  if (count == 0) return accumulate ? QBA_OK : zero_counts(n, H, C, P, (hipStream_t)stream);
+  if ((rc = need_program(ctx, n, "qba_sample_check"))) return rc;
+  QbaLaunch L{n, 1, (const QbaProgramSet *)ctx->prog_dev[n], seed, first, count, lists, ld,
+              H, C, P, ctx->stats, accumulate, (hipStream_t)stream};
+  return dispatch(ctx, L);
+}
+
+extern "C" int qba_check_counts(qba_ctx *ctx, int n, const uint8_t *lists, uint64_t count,
+                                uint64_t ld, int64_t *H, int64_t *C, int64_t *P, int accumulate,
+                                qba_stream stream) {
+  int rc = check_common(ctx, n, lists, count, ld, "qba_check_counts");
+  if (rc) return rc;
+  if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_check_counts: H, C and P are required");
+  if (count == 0) return accumulate ? QBA_OK : zero_counts(n, H, C, P, (hipStream_t)stream);
+  QbaLaunch L{n, 2, nullptr, 0, 0, count, const_cast<uint8_t *>(lists), ld,
+              H, C, P, ctx->stats, accumulate, (hipStream_t)stream};
+  return dispatch(ctx, L);
+}
+
+extern "C" int qba_reserve(qba_ctx *ctx, int n, int64_t max_blocks) {
+  if (!ctx || n < 1 || n > QBA_MAX_PARTIES || max_blocks < 1)
+    return qba_fail(QBA_EINVAL, "qba_reserve: bad arguments");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  return qba_ensure_slab(ctx, (size_t)max_blocks * nbins_of(n) * sizeof(uint32_t));
+}
+
+// ---------------------------------------------------------------------------
+// Philox KAT helper
+// ---------------------------------------------------------------------------
+__global__ void qba_k_philox(const uint32_t *__restrict__ ctr, int64_t n, uint32_t k0, uint32_t k1,
+                             uint32_t *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const QbaU4 r = qba_philox(ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3], k0, k1);
+  out[4 * i] = r.x;
+  out[4 * i + 1] = r.y;
+  out[4 * i + 2] = r.z;
+  out[4 * i + 3] = r.w;
+}
+
+extern "C" int qba_philox_dev(qba_ctx *ctx, const uint32_t *ctr, int64_t n, uint64_t key,
+                              uint32_t *out, qba_stream stream) {
+  if (!ctx || n < 0 || (n && (!ctr || !out))) return qba_fail(QBA_EINVAL, "qba_philox_dev: bad arguments");
+  if (n == 0) return QBA_OK;
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  hipLaunchKernelGGL(qba_k_philox, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, ctr, n, (uint32_t)key, (uint32_t)(key >> 32), out);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}

@@ -1,0 +1,289 @@
+"""Device engine: torch-tensor front end of libqba (include/qba.h).
+
+PyTorch is used only for device memory, streams and torch.distributed; every
+computation on lists, counts and statevectors runs in the HIP kernels of
+libqba.  Constructing an :class:`Engine` without the library or without a
+gfx950 GPU raises :class:`QbaError` -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import resource
+from ._lib import KIND_NOTQ, KIND_Q, MAX_PARTIES, QbaError, call, lib
+
+
+def _ptr(t: torch.Tensor) -> C.c_void_p:
+    return C.c_void_p(t.data_ptr())
+
+
+def _i32p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+@dataclass
+class Counts:
+    """Count-mode result of one pass (see qba.h): int64 device tensors."""
+
+    H: torch.Tensor  # [w][n+1][w]
+    C: torch.Tensor  # [w][n+1][n+1]
+    P: torch.Tensor  # [w]
+
+    def numpy(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        return self.H.cpu().numpy(), self.C.cpu().numpy(), self.P.cpu().numpy()
+
+
+class Engine:
+    """One libqba context bound to one GPU."""
+
+    def __init__(self, device: int = 0):
+        if not torch.cuda.is_available():
+            raise QbaError("no GPU visible: the qba engine has no CPU fallback")
+        self.device = torch.device("cuda", device)
+        self.index = device
+        handle = C.c_void_p()
+        torch.cuda.set_device(device)
+        call("qba_init", device, C.byref(handle))
+        self._ctx = handle
+        self._prepared: Dict[int, dict] = {}
+
+    # -- lifetime ----------------------------------------------------------
+    def close(self) -> None:
+        if self._ctx:
+            torch.cuda.synchronize(self.device)
+            call("qba_destroy", self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            if getattr(self, "_ctx", None):
+                lib().qba_destroy(self._ctx)
+        except Exception:
+            pass
+
+    @property
+    def ctx(self) -> C.c_void_p:
+        if not self._ctx:
+            raise QbaError("engine closed")
+        return self._ctx
+
+    def stream(self) -> C.c_void_p:
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -- sizes --------------------------------------------------------------
+    @staticmethod
+    def sizes(n: int) -> Tuple[int, int]:
+        nq = resource.n_qubits(n)
+        return nq, 1 << nq
+
+    @staticmethod
+    def _check_n(n: int) -> None:
+        if not 1 <= n <= MAX_PARTIES:
+            raise QbaError(f"n_parties={n} outside [1, {MAX_PARTIES}]")
+
+    # -- (A1/A2) resource preparation ------------------------------------------
+    def prepare(self, n: int, perm: Optional[Sequence[int]] = None) -> dict:
+        """Compile both reference circuits for n parties (tfg.py:15-65).
+
+        The Q circuit is built with permutation ``perm`` (default: identity);
+        its X gates are verified by the library to be the classical mask the
+        sampler redraws for every entry.
+        """
+        self._check_n(n)
+        if n in self._prepared and perm is None:
+            return self._prepared[n]
+        nq, _ = self.sizes(n)
+        notq = resource.notQCorrelated(n, nq)
+        q = resource.qCorrelated(n, nq, perm=list(range(1, n + 1)) if perm is None else perm)
+        g0 = np.ascontiguousarray(notq.triples())
+        g1 = np.ascontiguousarray(q.triples())
+        p1 = np.ascontiguousarray(q.perm.astype(np.int32))
+        call("qba_resource_compile", self.ctx, n, KIND_NOTQ, _i32p(g0), len(g0), None)
+        call("qba_resource_compile", self.ctx, n, KIND_Q, _i32p(g1), len(g1), _i32p(p1))
+        info = {"n": n, "nq": nq, "notq": self.program(n, KIND_NOTQ), "q": self.program(n, KIND_Q)}
+        self._prepared[n] = info
+        return info
+
+    def program(self, n: int, kind: int) -> dict:
+        nf = C.c_int32()
+        tl = C.c_int32()
+        desc = np.zeros((16, 6), np.int32)
+        cap = 8192
+        pat = np.zeros(cap, np.uint64)
+        apat = np.zeros(cap, np.uint64)
+        thr = np.zeros(cap, np.uint64)
+        u64p = C.POINTER(C.c_uint64)
+        call("qba_program_export", self.ctx, n, kind, C.byref(nf), _i32p(desc),
+             pat.ctypes.data_as(u64p), apat.ctypes.data_as(u64p), thr.ctypes.data_as(u64p), cap,
+             C.byref(tl))
+        t = tl.value
+        return {"nfac": nf.value, "desc": desc[: nf.value].copy(), "pat": pat[:t].copy(),
+                "apat": apat[:t].copy(), "thr": thr[:t].copy()}
+
+    # -- buffers -----------------------------------------------------------------
+    def alloc_lists(self, n: int, count: int) -> torch.Tensor:
+        ld = max(64, (count + 63) // 64 * 64)
+        return torch.empty((n + 1, ld), dtype=torch.uint8, device=self.device)
+
+    def alloc_counts(self, n: int) -> Counts:
+        _, w = self.sizes(n)
+        z = lambda *s: torch.zeros(s, dtype=torch.int64, device=self.device)  # noqa: E731
+        return Counts(z(w, n + 1, w), z(w, n + 1, n + 1), z(w))
+
+    @staticmethod
+    def _lists_ok(lists: torch.Tensor, n: int, count: int) -> int:
+        if lists.dtype != torch.uint8 or lists.dim() != 2 or lists.shape[0] != n + 1:
+            raise QbaError("lists must be a uint8 [n+1, ld] device tensor")
+        if lists.stride(1) != 1 or lists.shape[1] < count:
+            raise QbaError("lists rows must be contiguous and hold `count` entries")
+        return lists.stride(0)
+
+    # -- (A3/A4) sampling ---------------------------------------------------------
+    def sample(self, n: int, seed: int, first: int, count: int,
+               lists: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Lists of entries [first, first+count) (tfg.py:68-84, 128-129)."""
+        self.prepare(n)
+        if lists is None:
+            lists = self.alloc_lists(n, count)
+        ld = self._lists_ok(lists, n, count)
+        call("qba_sample", self.ctx, n, seed, first, count, _ptr(lists), ld, self.stream())
+        return lists
+
+    def sample_check(self, n: int, seed: int, first: int, count: int,
+                     lists: Optional[torch.Tensor] = None, counts: Optional[Counts] = None,
+                     accumulate: bool = False) -> Tuple[torch.Tensor, Counts]:
+        self.prepare(n)
+        if lists is None:
+            lists = self.alloc_lists(n, count)
+        if counts is None:
+            counts = self.alloc_counts(n)
+        ld = self._lists_ok(lists, n, count)
+        call("qba_sample_check", self.ctx, n, seed, first, count, _ptr(lists), ld,
+             _ptr(counts.H), _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
+        return lists, counts
+
+    # -- (A5-A8) count mode -------------------------------------------------------
+    def check_counts(self, lists: torch.Tensor, n: int, count: int,
+                     counts: Optional[Counts] = None, accumulate: bool = False) -> Counts:
+        self._check_n(n)
+        if counts is None:
+            counts = self.alloc_counts(n)
+        ld = self._lists_ok(lists, n, count)
+        call("qba_check_counts", self.ctx, n, _ptr(lists), count, ld, _ptr(counts.H),
+             _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
+        return counts
+
+    def last_stats(self) -> np.ndarray:
+        out = np.zeros(2, np.int64)
+        call("qba_last_stats", self.ctx, out.ctypes.data_as(C.POINTER(C.c_int64)))
+        return out
+
+    def reserve(self, n: int, max_blocks: int) -> None:
+        call("qba_reserve", self.ctx, n, max_blocks)
+
+    # -- (A5-A8) exact-order mode -----------------------------------------------
+    def to_device(self, arr) -> torch.Tensor:
+        return torch.as_tensor(np.ascontiguousarray(arr)).to(self.device, non_blocking=False)
+
+    @staticmethod
+    def to_host(t: torch.Tensor) -> np.ndarray:
+        return t.cpu().numpy()
+
+    def isq_indices(self, li: torch.Tensor, lc: torch.Tensor) -> np.ndarray:
+        """Ascending {k : Li[k] != Lc[k]} (tfg.py:327)."""
+        count = li.numel()
+        out = torch.empty(max(count, 1), dtype=torch.int64, device=self.device)
+        found = C.c_int64()
+        call("qba_isq_indices", self.ctx, _ptr(li), _ptr(lc), count, _ptr(out), count,
+             C.byref(found), self.stream())
+        return out[: found.value].cpu().numpy()
+
+    def select_eq(self, order: np.ndarray, lc: torch.Tensor, v: int) -> np.ndarray:
+        """[x for x in order if Lc[x] == v], order kept (tfg.py:182)."""
+        m = len(order)
+        if m == 0:
+            return np.zeros(0, np.int64)
+        d_order = self.to_device(np.asarray(order, dtype=np.int64))
+        out = torch.empty(m, dtype=torch.int64, device=self.device)
+        found = C.c_int64()
+        call("qba_select_eq", self.ctx, _ptr(d_order), m, _ptr(lc), int(v), _ptr(out),
+             C.byref(found), self.stream())
+        return out[: found.value].cpu().numpy()
+
+    def gather(self, li: torch.Tensor, order: np.ndarray) -> np.ndarray:
+        """Li[j] for j in order (tfg.py:189, 291)."""
+        m = len(order)
+        if m == 0:
+            return np.zeros(0, np.int64)
+        d_idx = self.to_device(np.asarray(order, dtype=np.int64))
+        out = torch.empty(m, dtype=torch.int64, device=self.device)
+        call("qba_gather", self.ctx, _ptr(li), li.numel(), _ptr(d_idx), m, _ptr(out), self.stream())
+        return out.cpu().numpy()
+
+    def consistent_rows(self, rows: np.ndarray, v: int, w: int) -> bool:
+        """Cond2 and Cond3 of tfg.py:93-98 over an (m, len) int64 matrix."""
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        m, ln = rows.shape
+        d = self.to_device(rows) if ln > 0 else torch.zeros(1, dtype=torch.int64, device=self.device)
+        ok = C.c_int32()
+        call("qba_consistent", self.ctx, _ptr(d), m, ln, int(v), int(w), C.byref(ok), self.stream())
+        return bool(ok.value)
+
+    # -- codec (rawS wire layout) ----------------------------------------------
+    def bits_to_values(self, raw: torch.Tensor, count: int, nq: int) -> torch.Tensor:
+        out = torch.empty(max(count, 1), dtype=torch.uint8, device=self.device)
+        call("qba_bits_to_values", self.ctx, _ptr(raw), count, nq, _ptr(out), self.stream())
+        return out[:count]
+
+    def values_to_bits(self, values: torch.Tensor, count: int, nq: int) -> torch.Tensor:
+        out = torch.empty(max(count * nq, 1), dtype=torch.int64, device=self.device)
+        call("qba_values_to_bits", self.ctx, _ptr(values), count, nq, _ptr(out), self.stream())
+        return out[: count * nq]
+
+    # -- statevector -------------------------------------------------------------
+    def statevector(self, nqubits: int, gates: np.ndarray,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        sv = out if out is not None else torch.empty(1 << nqubits, dtype=torch.float64, device=self.device)
+        g = np.ascontiguousarray(gates, dtype=np.int32).reshape(-1, 3)
+        call("qba_sv_init", self.ctx, _ptr(sv), nqubits, self.stream())
+        call("qba_sv_apply", self.ctx, _ptr(sv), nqubits, _i32p(g), len(g), self.stream())
+        return sv
+
+    def apply_gates(self, sv: torch.Tensor, nqubits: int, gates: np.ndarray) -> None:
+        g = np.ascontiguousarray(gates, dtype=np.int32).reshape(-1, 3)
+        call("qba_sv_apply", self.ctx, _ptr(sv), nqubits, _i32p(g), len(g), self.stream())
+
+    def support(self, sv: torch.Tensor, nqubits: int, eps: float = 1e-24,
+                cap: int = 1 << 20) -> Tuple[np.ndarray, np.ndarray]:
+        idx = torch.empty(cap, dtype=torch.int64, device=self.device)
+        prob = torch.empty(cap, dtype=torch.float64, device=self.device)
+        cnt = C.c_int64()
+        call("qba_sv_support", self.ctx, _ptr(sv), nqubits, float(eps), _ptr(idx), _ptr(prob), cap,
+             C.byref(cnt), self.stream())
+        k = min(cnt.value, cap)
+        if cnt.value > cap:
+            raise QbaError(f"support of {cnt.value} outcomes exceeds cap={cap}")
+        return idx[:k].cpu().numpy(), prob[:k].cpu().numpy()
+
+    # -- test helpers -------------------------------------------------------------
+    def philox(self, ctr: np.ndarray, key: int) -> np.ndarray:
+        ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
+        d_ctr = self.to_device(ctr.view(np.int32))
+        out = torch.empty_like(d_ctr)
+        call("qba_philox_dev", self.ctx, _ptr(d_ctr), len(ctr), int(key), _ptr(out), self.stream())
+        return out.cpu().numpy().view(np.uint32)
+
+
+def alias_build(probs: Sequence[float]) -> Tuple[np.ndarray, np.ndarray]:
+    """Host Vose alias table (exported for tests): (thr u64 in [0, 2^32], alias i32)."""
+    p = np.ascontiguousarray(probs, dtype=np.float64)
+    thr = np.zeros(len(p), np.uint64)
+    alias = np.zeros(len(p), np.int32)
+    call("qba_alias_build", p.ctypes.data_as(C.POINTER(C.c_double)), len(p),
+         thr.ctypes.data_as(C.POINTER(C.c_uint64)), alias.ctypes.data_as(C.POINTER(C.c_int32)))
+    return thr, alias

@@ -1,0 +1,424 @@
+"""tfg.py-compatible protocol host (exact mode).
+
+This mirrors the reference's operator interface -- the same function names,
+argument meaning, message format, random-number call order and error
+behaviour (tfg.py:87-363) -- while every per-element operation on the lists
+runs in libqba's HIP kernels through :class:`~.engine.Engine`:
+
+======================  ==========================  ===============================
+reference               here                        device work
+======================  ==========================  ===============================
+generacionListas  :68   :func:`generacionListas`    qba_sample + qba_values_to_bits
+measure_to_ints   :128  :func:`measure_to_ints`     qba_bits_to_values
+isQCorrList       :327  :meth:`Party.commander_setup`  qba_isq_indices
+P filter          :182  :meth:`Party.p_for`         qba_select_eq
+own tuple    :189, :291 :meth:`Party.own_tuple`     qba_gather
+consistent        :87   :func:`consistent`          qba_consistent (Cond1 on host)
+======================  ==========================  ===============================
+
+Exactness: the reference builds each tuple in its process's own CPython
+set-iteration order, so the host keeps real Python sets and
+performs the same list(P) -> wire -> set(buff) hops; the device receives the
+resulting index orders.  With identical injected lists, rank seeds and
+delivery order the decisions, V_i sets and accept/reject counts equal the
+reference's (tests/test_protocol.py against tests/golden/protocol.json).
+
+Rounds use the host's comm: real mpi4py under ``mpiexec``, or
+:class:`~.comm.LocalWorld` threads (barrier-epoch delivery, comm.py).
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+
+from . import comm as comm_mod
+from .resource import n_qubits
+
+INT = comm_mod.INT
+ANY_SOURCE = comm_mod.ANY_SOURCE
+
+
+# ---------------------------------------------------------------------------
+# module-level functions with the reference's names
+# ---------------------------------------------------------------------------
+def generacionListas(nParties, size, nQubits, w, engine=None, seed=0, lists=None):
+    """rawS: (n+1, nQubits*size) int64 bits, MSB first per value (tfg.py:68-84).
+
+    Lists are drawn on the device (Philox keyed by entry index, ``seed``), or
+    taken from ``lists`` (an injected (n+1, size) value array), then encoded
+    to the reference's one-int64-per-bit wire layout on the device.
+    """
+    if engine is None:
+        raise RuntimeError("generacionListas needs an Engine (no CPU fallback)")
+    if lists is None:
+        dev = engine.sample(nParties, seed, 0, size)
+    else:
+        arr = np.ascontiguousarray(lists, dtype=np.uint8)
+        if arr.shape != (nParties + 1, size):
+            raise ValueError(f"injected lists must have shape {(nParties + 1, size)}")
+        dev = engine.to_device(arr)
+    out = np.empty((nParties + 1, nQubits * size), np.int64)
+    for g in range(nParties + 1):
+        out[g] = engine.to_host(engine.values_to_bits(dev[g, :size], size, nQubits))
+    return out
+
+
+def measure_to_ints(raw, sizeL, nQubits, engine=None):
+    """MSB-first nQubits-bit groups -> list of ints (tfg.py:128-129), on the device."""
+    if engine is None:
+        raise RuntimeError("measure_to_ints needs an Engine (no CPU fallback)")
+    vals = engine.bits_to_values(engine.to_device(np.asarray(raw, dtype=np.int64)), sizeL, nQubits)
+    return engine.to_host(vals).astype(np.int64).tolist()
+
+
+def consistent(v, L, w, engine=None):
+    """consistent(v, L, w) of tfg.py:87-98.
+
+    Cond1 (equal lengths; StopIteration on an empty L, as ``next(iter(L))``)
+    is host bookkeeping; Cond2 and Cond3 run in qba_consistent.
+    """
+    it = iter(L)
+    length = len(next(it))
+    if any(len(t) != length for t in it):
+        return False
+    if engine is None:
+        raise RuntimeError("consistent needs an Engine (no CPU fallback)")
+    rows = np.array([list(t) for t in L], dtype=np.int64).reshape(len(L), length)
+    return engine.consistent_rows(rows, int(v), int(w))
+
+
+def decide_order(Vi, v, is_comm):
+    """tfg.py:303-306: the commander keeps its v, a lieutenant takes min(V_i)."""
+    return v if is_comm else min(Vi)
+
+
+# ---------------------------------------------------------------------------
+# wire format of a (P, v, L) packet (tfg.py:199-263)
+# ---------------------------------------------------------------------------
+def send_pvl(comm, rank, dest, P, v, L, is_biz, log=None):
+    if log:
+        log(f"[{'B' if is_biz else ''}{rank} -> {dest}] Sending", (P, (v, L)))
+    msgs = [np.array(len(P), dtype=np.int64),
+            np.array(list(P), dtype=np.int64),
+            np.array(v, dtype=np.int64),
+            np.array(len(L), dtype=np.int64)]
+    for sub in L:
+        msgs.append(np.array(len(sub), dtype=np.int64))
+        msgs.append(np.array(sub, dtype=np.int64))
+    reqs = [comm.Isend([m, INT], dest=dest, tag=t) for t, m in enumerate(msgs, start=1)]
+    for r in reqs:
+        r.Wait()
+    if log:
+        log(f"[{'B' if is_biz else ''}{rank} -> {dest}] Sent packet!")
+
+
+def _recv_array(comm, src, tag, n):
+    buf = np.empty(n, dtype=np.int64)
+    comm.Irecv([buf, INT], source=src, tag=tag).Wait()
+    return buf
+
+
+def recv_pvl(comm, rank, src):
+    """Receive one packet; P and L are rebuilt as sets from the wire order."""
+    n_p = int(_recv_array(comm, src, 1, 1)[0])
+    P = set(_recv_array(comm, src, 2, n_p))
+    v = _recv_array(comm, src, 3, 1)[0]
+    n_l = int(_recv_array(comm, src, 4, 1)[0])
+    L = set()
+    for i in range(n_l):
+        ln = int(_recv_array(comm, src, 5 + 2 * i, 1)[0])
+        L.add(tuple(_recv_array(comm, src, 6 + 2 * i, ln)))
+    return P, v, L
+
+
+# ---------------------------------------------------------------------------
+# one rank
+# ---------------------------------------------------------------------------
+@dataclass
+class PartyStats:
+    accept: int = 0
+    reject: int = 0
+    sent: int = 0
+
+
+class _Locked:
+    """Serialises an Engine shared by the threads of a LocalWorld."""
+
+    def __init__(self, engine, lock):
+        self._engine, self._lock = engine, lock
+
+    def __getattr__(self, name):
+        attr = getattr(self._engine, name)
+        if not callable(attr):
+            return attr
+
+        def call(*a, **k):
+            with self._lock:
+                return attr(*a, **k)
+        return call
+
+
+class Party:
+    """State of one rank: 0 = the QSD, 1 = commander, >= 2 = lieutenants."""
+
+    def __init__(self, comm, sizeL, nDishonest, engine, rng, log=None, lists=None, seed=0):
+        self.comm = comm
+        self.rank = comm.Get_rank()
+        self.n = comm.Get_size() - 1
+        self.nq = n_qubits(self.n)
+        self.w = 2 ** self.nq
+        self.sizeL = sizeL
+        self.n_dis = nDishonest
+        self.engine = engine
+        self.rng = rng
+        self.log = log
+        self.inject = lists
+        self.seed = seed
+        self.Vi: set = set()
+        self.stats = PartyStats()
+        self.li = None  # device row of this rank's list
+        self.lc = None  # device row of Lc (commander only)
+        self.dishonest = False
+        self.dishonest_ids = None
+        self._p_cache: Dict[int, List[int]] = {}
+        self.tolerate_empty_vi = False  # run_local: record the reference's ValueError
+        self.empty_vi_error = False
+
+    def say(self, *args):
+        if self.log:
+            self.log(*args)
+
+    # tfg.py:101-125
+    def dishonest_comm(self):
+        c, n = self.comm, self.n
+        if self.rank == 0:
+            ids = self.rng.choice(np.arange(1, n + 1), self.n_dis, replace=False)
+            reqs = [c.Isend([np.array(i in ids, dtype=np.int64), INT], dest=i) for i in range(1, n + 1)]
+            for r in reqs:
+                r.Wait()
+            self.dishonest_ids = ids
+            return ids
+        self.dishonest = bool(_recv_array(c, 0, comm_mod.ANY_TAG, 1)[0])
+        self.say(f"[{self.rank}] I'm {'dis' if self.dishonest else ''}honest")
+        return self.dishonest
+
+    # tfg.py:132-163
+    def particle_comm(self):
+        c, n, nq, sl = self.comm, self.n, self.nq, self.sizeL
+        if self.rank == 0:
+            self.say("|W| =", self.w)
+            raw = generacionListas(n, sl, nq, self.w, self.engine, self.seed, self.inject)
+            reqs = [c.Isend([raw[0], INT], dest=1)]
+            reqs += [c.Isend([raw[g], INT], dest=g) for g in range(1, n + 1)]
+            for r in reqs:
+                r.Wait()
+            return
+        mine = np.empty(nq * sl, np.int64)
+        req = c.Irecv([mine, INT], source=0)  # posted first: gets rawS[0] at rank 1
+        if self.rank == 1:
+            extra = np.empty(nq * sl, np.int64)
+            c.Irecv([extra, INT], source=0).Wait()
+            self.lc = self._decode(extra)
+        req.Wait()
+        self.li = self._decode(mine)
+
+    def _decode(self, raw):
+        return self.engine.bits_to_values(self.engine.to_device(raw), self.sizeL, self.nq)
+
+    # tfg.py:327-330
+    def commander_setup(self):
+        self.isq = set(self.engine.isq_indices(self.li, self.lc).tolist())
+        self.say("isQCorr = ", self.isq)
+        self.v = self.rng.randint(self.w)
+        self.say("v =", self.v)
+
+    def p_for(self, v) -> set:
+        """{x for x in isQCorr if Lc[x] == v} in isQCorr's iteration order (tfg.py:182)."""
+        key = int(v)
+        if key not in self._p_cache:
+            order = np.fromiter(self.isq, dtype=np.int64, count=len(self.isq))
+            self._p_cache[key] = self.engine.select_eq(order, self.lc, key).tolist()
+        return set(self._p_cache[key])
+
+    def own_tuple(self, P) -> tuple:
+        """tuple(Li[j] for j in P) in this process's iteration order of P (tfg.py:189, 291)."""
+        order = np.fromiter(P, dtype=np.int64, count=len(P))
+        return tuple(self.engine.gather(self.li, order).tolist())
+
+    def check(self, v, L) -> bool:
+        ok = consistent(v, L, self.w, self.engine)
+        if ok:
+            self.stats.accept += 1
+        else:
+            self.stats.reject += 1
+        return ok
+
+    def send(self, dest, P, v, L):
+        self.stats.sent += 1
+        send_pvl(self.comm, self.rank, dest, P, v, L, self.dishonest, self.log)
+
+    # tfg.py:166-196
+    def comm_broadcast(self):
+        if self.rank == 1:
+            v = self.v
+            if self.dishonest:
+                v1 = self.rng.randint(self.w)
+                v2 = self.rng.randint(self.w)
+                while v2 == v1:
+                    v2 = self.rng.randint(self.w)
+            for dest in range(2, self.n + 1):
+                if self.dishonest:
+                    v = v1 if dest <= int((self.n + 1) / 2) else v2
+                self.send(dest, self.p_for(v), v, set())
+        elif self.rank > 1:
+            P, v, L = recv_pvl(self.comm, self.rank, 1)
+            L.add(self.own_tuple(P))
+            self.say(f"[{self.rank}] L = {L}")
+            if self.check(v, L):
+                self.Vi.add(v)
+                self.lieu_broadcast(P, v, L)
+
+    # tfg.py:266-286
+    def lieu_broadcast(self, P, v, L):
+        for dest in range(2, self.n + 1):
+            if dest == self.rank:
+                continue
+            go = 1
+            if self.dishonest:
+                action = self.rng.randint(4)
+                if action == 0:
+                    go = self.rng.randint(2)
+                    self.say(f"The action for general {self.rank} is: maybe not sending inf {go}")
+                elif action == 1:
+                    v = self.rng.randint(self.n + 1)
+                    self.say(f"The action for general {self.rank} is: sending order {v}")
+                elif action == 2:
+                    P.clear()
+                    self.say(f"The action for general {self.rank} is: empty P {P}")
+                else:
+                    L.clear()
+                    self.say(f"The action for general {self.rank} is: empy L {L}")
+            if go:
+                self.send(dest, P, v, L)
+
+    # tfg.py:289-300
+    def lieu_receive(self, P, v, L, rnd):
+        L.add(self.own_tuple(P))
+        if self.check(v, L) and v not in self.Vi and len(L) == rnd + 1:
+            self.Vi.add(v)
+            if rnd <= self.n_dis:
+                self.lieu_broadcast(P, v, L)
+
+    # tfg.py:309-363
+    def run(self) -> Optional[dict]:
+        c = self.comm
+        self.dishonest_comm()
+        self.particle_comm()
+        self.v = None
+        if self.rank == 1:
+            self.commander_setup()
+        self.comm_broadcast()
+        c.Barrier()
+        status = comm_mod.Status() if isinstance(c, comm_mod.LocalComm) else _mpi_status(c)
+        for rnd in range(1, self.n_dis + 2):
+            if self.rank > 1:
+                inbox = []
+                while c.Iprobe(source=ANY_SOURCE, status=status):
+                    inbox.append(recv_pvl(c, self.rank, status.Get_source()))
+                for P, v, L in inbox:
+                    self.lieu_receive(P, v, L, rnd)
+            c.Barrier()
+        if self.rank > 1 and not self.dishonest:
+            self.say(f"[{self.rank}] V{self.rank} = {self.Vi}")
+        if self.rank != 0:
+            try:
+                d = decide_order(self.Vi, self.v, self.rank == 1)
+            except ValueError:  # min(set()) on an empty V_i (tfg.py:306)
+                if not self.tolerate_empty_vi:
+                    raise
+                self.empty_vi_error, d = True, -1
+            c.Send([np.array(d, dtype=np.int64), INT], dest=0)
+            return None
+        result = np.empty(self.n, dtype=np.int64)
+        for src in range(1, self.n + 1):
+            result[src - 1] = _recv_array(c, src, comm_mod.ANY_TAG, 1)[0]
+        ids = self.dishonest_ids
+        honest = {int(result[i]) for i in range(self.n) if i + 1 not in ids}
+        self.say("Decisions:", result)
+        self.say("Dishonests:", ids)
+        self.say("Success:", len(honest) == 1)
+        return {"decisions": result.tolist(), "dishonest": sorted(int(x) for x in ids),
+                "success": len(honest) == 1}
+
+
+def _mpi_status(c):
+    from mpi4py import MPI  # type: ignore  # noqa: F401  (real MPI only)
+    return MPI.Status()
+
+
+def QBA(sizeL, nDishonest, engine=None, comm=None, rng=None, log=print, lists=None, seed=0):
+    """One rank of the protocol (tfg.py:309-363): call it on every rank.
+
+    ``comm`` defaults to ``mpi4py.MPI.COMM_WORLD``; ``rng`` to ``np.random``
+    (the reference's global generator); ``lists`` injects (n+1, sizeL) values
+    in place of sampling.  Returns the result dict on rank 0, None elsewhere.
+    """
+    if comm is None:
+        mpi = comm_mod.mpi_world()
+        if mpi is None:
+            raise RuntimeError("mpi4py is not installed: use run_local() for an in-process run")
+        comm = mpi.COMM_WORLD
+    party = Party(comm, sizeL, nDishonest, engine, rng if rng is not None else np.random, log, lists, seed)
+    return party.run()
+
+
+@dataclass
+class LocalRun:
+    result: Optional[dict]
+    V: Dict[int, List[int]] = field(default_factory=dict)
+    accept: List[int] = field(default_factory=list)
+    reject: List[int] = field(default_factory=list)
+    sent: List[int] = field(default_factory=list)
+    messages: int = 0
+    bytes: int = 0
+    error: Optional[str] = None
+    error_ranks: List[int] = field(default_factory=list)
+
+
+def run_local(n_parties: int, sizeL: int, nDishonest: int, engine, seed: int = 0,
+              lists: Optional[np.ndarray] = None, log: Optional[Callable] = None,
+              list_seed: Optional[int] = None, timeout: float = 120.0) -> LocalRun:
+    """Run all n+1 ranks in-process on a LocalWorld.
+
+    Rank r draws from ``np.random.RandomState(seed*1000 + r)`` (the fixtures'
+    convention).  A lieutenant whose V_i is empty raises ValueError in
+    decide_order exactly like the reference; here it is recorded in
+    ``error``/``error_ranks`` and the run completes with decision -1.
+    """
+    world = comm_mod.LocalWorld(n_parties + 1, timeout=timeout)
+    shared = _Locked(engine, threading.RLock())
+    parties: List[Optional[Party]] = [None] * (n_parties + 1)
+
+    def body(c):
+        rs = np.random.RandomState(seed * 1000 + c.rank)
+        p = Party(c, sizeL, nDishonest, shared, rs, log, lists,
+                  seed if list_seed is None else list_seed)
+        p.tolerate_empty_vi = True
+        parties[c.rank] = p
+        return p.run()
+
+    res = world.run(body)
+    out = LocalRun(result=res[0], messages=world.sent_messages, bytes=world.sent_bytes)
+    for p in parties:
+        out.accept.append(p.stats.accept)
+        out.reject.append(p.stats.reject)
+        out.sent.append(p.stats.sent)
+        if p.rank > 1 and not p.dishonest:
+            out.V[p.rank] = sorted(int(x) for x in p.Vi)
+    out.error_ranks = [p.rank for p in parties if p.empty_vi_error]
+    if out.error_ranks:
+        out.error = "ValueError"
+    return out
