@@ -34,3 +34,9 @@ class OracleEngine:
 
     def consistent_rows(self, rows, v, w):
         return orc.consistent(v, {tuple(r) for r in rows.tolist()}, w) if len(rows) else True
+
+    def count_tables(self, n, sizeL, seed=0, lists=None, chunk=None):
+        if lists is None:
+            raise NotImplementedError("the oracle engine only checks injected lists")
+        H, C, P = orc.counts(np.asarray(lists), n)
+        return np.concatenate([H.ravel(), C.ravel(), P.ravel()])

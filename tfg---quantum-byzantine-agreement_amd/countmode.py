@@ -1,0 +1,142 @@
+"""Count-mode protocol: decisions from the device's count histograms.
+
+At large sizeL the reference's packets are impractical (P as int64 index
+lists is ~250 MB per packet at n=11, sizeL=1e9).  Count mode
+keeps the protocol rounds, random-number order and acceptance rules of
+tfg.py:166-363 exactly, but in CANONICAL ORDER (every party gathers P in
+ascending index order) and with compact packets:
+
+* the lists never leave the device: one ``qba_sample_check`` pass (chunked,
+  sharded over GPUs when there are several) yields
+      H[u][g][x] = #{k in P_u : L_g[k] = x}
+      C[u][g][h] = #{k in P_u : L_g[k] = L_h[k]}        P[u] = |P_u|
+  with P_u = {k : L0[k] != L1[k], Lc[k] = u}  (tfg.py:182, 327);
+* P travels as its value u (or "cleared"); a tuple L_g[P_u] travels as the
+  descriptor (u, g), canonicalised so that equal tuples compare equal
+  (C[u][g][h] = |P_u|), which preserves the reference's set de-duplication;
+* consistent(v, L, w) (tfg.py:87-98) is exact from the counts:
+      Cond1: all descriptors have the same length (|P_u| or 0),
+      Cond2: H[u][g][v] == 0 for every tuple (values are always in [0, w)),
+      Cond3: C[u][g][h] == 0 for every pair of distinct tuples.
+
+tests/test_countmode.py checks decisions, V_i and accept/reject counts
+against the reference run with sorted sets (tests/golden/protocol.json,
+"canonical").
+"""
+from __future__ import annotations
+
+import itertools
+from typing import Optional
+
+import numpy as np
+
+from . import comm as comm_mod
+from .protocol import INT, Party, _recv_array
+
+EMPTY = ()
+
+
+class CountTables:
+    """H, C, P of one run (host copies) and the descriptor algebra."""
+
+    def __init__(self, n: int, flat: np.ndarray):
+        self.n = n
+        self.w = 1 << int(n).bit_length()
+        w, g = self.w, n + 1
+        h, c = w * g * w, w * g * g
+        flat = np.asarray(flat, dtype=np.int64)
+        self.H = flat[:h].reshape(w, g, w)
+        self.C = flat[h:h + c].reshape(w, g, g)
+        self.P = flat[h + c:h + c + w]
+        self.flat = flat
+
+    def desc(self, g: int, u: Optional[int]):
+        """Canonical descriptor of tuple(L_g[j] for j in sorted(P_u))."""
+        if u is None or self.P[u] == 0:
+            return EMPTY
+        full = self.P[u]
+        rep = next(h for h in range(self.n + 1) if self.C[u, g, h] == full)
+        return (int(u), int(rep))
+
+    def length(self, d) -> int:
+        return 0 if d == EMPTY else int(self.P[d[0]])
+
+    def consistent(self, v, L) -> bool:
+        it = iter(L)
+        first = next(it)  # StopIteration on an empty L, as tfg.py:90
+        n0 = self.length(first)
+        if any(self.length(d) != n0 for d in it):
+            return False
+        descs = [d for d in L if d != EMPTY]
+        if not descs:
+            return True
+        if len({d[0] for d in descs}) != 1:
+            raise AssertionError("tuples over different P in one packet")
+        v = int(v)
+        # every list value lies in [0, w), so Cond2 can only fail through x == v
+        if 0 <= v < self.w and any(self.H[u, g, v] != 0 for u, g in descs):
+            return False
+        return all(self.C[a[0], a[1], b[1]] == 0 for a, b in itertools.combinations(descs, 2))
+
+
+class PRef:
+    """The P object of a packet: P_u, mutable only by clear() (tfg.py:280)."""
+
+    __slots__ = ("u",)
+
+    def __init__(self, u: Optional[int]):
+        self.u = u
+
+    def clear(self):
+        self.u = None
+
+
+class CountParty(Party):
+    """A rank of the count-mode protocol (same rounds and RNG use as Party)."""
+
+    chunk = 1 << 27
+
+    def particle_comm(self):
+        c, n = self.comm, self.n
+        w, g = 1 << int(n).bit_length(), n + 1
+        size = w * g * w + w * g * g + w
+        if self.rank == 0:
+            self.say("|W| =", self.w)
+            flat = self.engine.count_tables(n, self.sizeL, self.seed, self.inject, self.chunk)
+            self.tables = CountTables(n, flat)
+            reqs = [c.Isend([self.tables.flat, INT], dest=r) for r in range(1, n + 1)]
+            for r in reqs:
+                r.Wait()
+            return
+        self.tables = CountTables(n, _recv_array(c, 0, comm_mod.ANY_TAG, size))
+
+    def commander_setup(self):
+        self.v = self.rng.randint(self.w)
+        self.say("v =", self.v)
+
+    def p_for(self, v):
+        return PRef(int(v))
+
+    def own_tuple(self, P):
+        return self.tables.desc(self.rank, P.u)
+
+    def check(self, v, L) -> bool:
+        ok = self.tables.consistent(v, L)
+        if ok:
+            self.stats.accept += 1
+        else:
+            self.stats.reject += 1
+        return ok
+
+    def send(self, dest, P, v, L):
+        self.stats.sent += 1
+        pairs = np.array([x for d in L for x in (d if d != EMPTY else (-1, -1))], dtype=np.int64)
+        head = np.array([-1 if P.u is None else P.u, int(v), len(L)], dtype=np.int64)
+        self.comm.Isend([head, INT], dest=dest, tag=1).Wait()
+        self.comm.Isend([pairs, INT], dest=dest, tag=2).Wait()
+
+    def recv(self, src):
+        head = _recv_array(self.comm, src, 1, 3)
+        pairs = _recv_array(self.comm, src, 2, 2 * int(head[2])).reshape(-1, 2)
+        L = {EMPTY if a < 0 else (int(a), int(b)) for a, b in pairs.tolist()}
+        return PRef(None if head[0] < 0 else int(head[0])), int(head[1]), L

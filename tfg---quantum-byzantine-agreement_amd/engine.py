@@ -178,6 +178,35 @@ class Engine:
              _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
         return counts
 
+    def count_tables(self, n: int, sizeL: int, seed: int = 0, lists: Optional[np.ndarray] = None,
+                     chunk: int = 1 << 27) -> np.ndarray:
+        """Flat int64 [H | C | P] over sizeL entries: injected host lists are
+        checked on the device, otherwise entries are sampled and checked in
+        chunks of `chunk` (lists are written once to a reused buffer)."""
+        self._check_n(n)
+        _, w = self.sizes(n)
+        g = n + 1
+        h, c = w * g * w, w * g * g
+        flat = torch.zeros(h + c + w, dtype=torch.int64, device=self.device)
+        counts = Counts(flat[:h].view(w, g, w), flat[h:h + c].view(w, g, g), flat[h + c:])
+        if lists is not None:
+            arr = np.ascontiguousarray(lists, dtype=np.uint8)
+            if arr.shape != (g, sizeL):
+                raise QbaError(f"lists must have shape {(g, sizeL)}")
+            dev = self.alloc_lists(n, sizeL)
+            dev[:, :sizeL] = torch.from_numpy(arr).to(self.device)
+            self.check_counts(dev, n, sizeL, counts)
+        else:
+            buf = self.alloc_lists(n, min(chunk, max(sizeL, 1)))
+            for first in range(0, sizeL, chunk):
+                self.sample_check(n, seed, first, min(chunk, sizeL - first), buf, counts,
+                                  accumulate=first > 0)
+        out = flat.cpu().numpy()
+        if sizeL and self.last_stats()[0] != 0:
+            raise QbaError("lists hold values >= w at Q-correlated positions: count mode "
+                           "cannot evaluate them (the reference never produces such lists)")
+        return out
+
     def last_stats(self) -> np.ndarray:
         out = np.zeros(2, np.int64)
         call("qba_last_stats", self.ctx, out.ctypes.data_as(C.POINTER(C.c_int64)))

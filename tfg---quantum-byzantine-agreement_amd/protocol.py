@@ -260,6 +260,9 @@ class Party:
         self.stats.sent += 1
         send_pvl(self.comm, self.rank, dest, P, v, L, self.dishonest, self.log)
 
+    def recv(self, src):
+        return recv_pvl(self.comm, self.rank, src)
+
     # tfg.py:166-196
     def comm_broadcast(self):
         if self.rank == 1:
@@ -274,7 +277,7 @@ class Party:
                     v = v1 if dest <= int((self.n + 1) / 2) else v2
                 self.send(dest, self.p_for(v), v, set())
         elif self.rank > 1:
-            P, v, L = recv_pvl(self.comm, self.rank, 1)
+            P, v, L = self.recv(1)
             L.add(self.own_tuple(P))
             self.say(f"[{self.rank}] L = {L}")
             if self.check(v, L):
@@ -327,7 +330,7 @@ class Party:
             if self.rank > 1:
                 inbox = []
                 while c.Iprobe(source=ANY_SOURCE, status=status):
-                    inbox.append(recv_pvl(c, self.rank, status.Get_source()))
+                    inbox.append(self.recv(status.Get_source()))
                 for P, v, L in inbox:
                     self.lieu_receive(P, v, L, rnd)
             c.Barrier()
@@ -390,7 +393,8 @@ class LocalRun:
 
 def run_local(n_parties: int, sizeL: int, nDishonest: int, engine, seed: int = 0,
               lists: Optional[np.ndarray] = None, log: Optional[Callable] = None,
-              list_seed: Optional[int] = None, timeout: float = 120.0) -> LocalRun:
+              list_seed: Optional[int] = None, timeout: float = 120.0,
+              party_cls=None, party_kwargs: Optional[dict] = None) -> LocalRun:
     """Run all n+1 ranks in-process on a LocalWorld.
 
     Rank r draws from ``np.random.RandomState(seed*1000 + r)`` (the fixtures'
@@ -404,8 +408,8 @@ def run_local(n_parties: int, sizeL: int, nDishonest: int, engine, seed: int = 0
 
     def body(c):
         rs = np.random.RandomState(seed * 1000 + c.rank)
-        p = Party(c, sizeL, nDishonest, shared, rs, log, lists,
-                  seed if list_seed is None else list_seed)
+        p = (party_cls or Party)(c, sizeL, nDishonest, shared, rs, log, lists,
+                                 seed if list_seed is None else list_seed, **(party_kwargs or {}))
         p.tolerate_empty_vi = True
         parties[c.rank] = p
         return p.run()
