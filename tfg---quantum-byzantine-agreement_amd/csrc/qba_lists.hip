@@ -39,14 +39,24 @@ struct QCfg {
 // ---------------------------------------------------------------------------
 // random words of one entry (schedule documented in qba_internal.h)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t qba_word(int kind, int k, const QbaU4 &x, uint32_t elo,
-                                             uint32_t ehi, uint32_t k0, uint32_t k1) {
-  const int base = kind ? 1 : 3;
-  if (k < base) return k == 0 ? x.y : (k == 1 ? x.z : x.w);
-  const int kk = k - base;
+// Words beyond block 0 (only programs with many or non-uniform factors):
+// kept out of line so the common path stays small.
+__device__ __attribute__((noinline)) uint32_t qba_word_ext(int kk, uint32_t elo, uint32_t ehi,
+                                                           uint32_t k0, uint32_t k1) {
   const QbaU4 y = qba_philox(elo, ehi, 1u + (uint32_t)(kk >> 2), 0u, k0, k1);
   const int s = kk & 3;
   return s == 0 ? y.x : (s == 1 ? y.y : (s == 2 ? y.z : y.w));
+}
+
+// Word k of the table stream (k is wave-uniform).  Block-0 words are picked
+// with uniform masks so the selection stays in registers.
+__device__ __forceinline__ uint32_t qba_word(int kind, int k, const QbaU4 &x, uint32_t elo,
+                                             uint32_t ehi, uint32_t k0, uint32_t k1) {
+  k = __builtin_amdgcn_readfirstlane(k);
+  const int base = kind ? 1 : 3;
+  if (k >= base) return qba_word_ext(k - base, elo, ehi, k0, k1);
+  const uint32_t m0 = k == 0 ? ~0u : 0u, m1 = k == 1 ? ~0u : 0u, m2 = k == 2 ? ~0u : 0u;
+  return (x.y & m0) | (x.z & m1) | (x.w & m2);
 }
 
 template <typename Out>
