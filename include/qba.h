@@ -121,6 +121,15 @@ QBA_API int qba_sample_check(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_
                      uint64_t count, uint8_t *lists_dev, uint64_t ld, int64_t *H_dev,
                      int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);
 
+/* Batched independent runs (BASELINE configs[3]: 4096 independent 7-party
+ * instances per GPU).  Instance i uses Philox key seed_base + i over entries
+ * [0, count); its lists start at lists_dev + i*inst_stride (rows ld apart) and
+ * its counts at H_dev + i*w*(n+1)*w, C_dev + i*w*(n+1)^2, P_dev + i*w. */
+QBA_API int qba_sample_check_batched(qba_ctx *ctx, int n_parties, uint64_t seed_base,
+                                     int64_t n_instances, uint64_t count, uint8_t *lists_dev,
+                                     uint64_t ld, uint64_t inst_stride, int64_t *H_dev,
+                                     int64_t *C_dev, int64_t *P_dev, qba_stream stream);
+
 /* ---- (A5-A8) checks, exact-order mode (bit-exact protocol parity) --------------- */
 /* isQCorrList = {k : Li[k] != Lc[k]} (tfg.py:327) as ascending indices.
  * *count_host receives the number found; at most `cap` are written. Synchronous. */

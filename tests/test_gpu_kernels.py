@@ -285,3 +285,19 @@ def test_log_tuples_exact_order(engine):
             assert any(hits), (info["file"], p["src"], p["dst"])
             checked += 1
     assert checked == 205
+
+
+def test_batched_instances(engine):
+    """Batched mode (configs[3] shape, scaled down): instance i == an ordinary
+    run with seed base+i, bit for bit, lists and counts."""
+    n, n_inst, count, base = 7, 37, 3001, 1000
+    info = engine.prepare(n)
+    lists, c = engine.sample_check_batched(n, base, n_inst, count)
+    torch.cuda.synchronize()
+    for i in (0, 1, 17, 36):
+        ref = oracle_lib.sample(n, base + i, 0, count, info["notq"], info["q"])
+        assert np.array_equal(lists[i, :, :count].cpu().numpy(), ref)
+        H, C, P, bad = oracle_lib.counts(ref, n)
+        assert np.array_equal(c.H[i].cpu().numpy(), H)
+        assert np.array_equal(c.C[i].cpu().numpy(), C)
+        assert np.array_equal(c.P[i].cpu().numpy(), P)

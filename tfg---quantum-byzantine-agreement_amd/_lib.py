@@ -40,6 +40,7 @@ SIGNATURES = {
     "qba_check_counts": [_p, C.c_int, _p, _u64, _u64, _p, _p, _p, C.c_int, _p],
     "qba_last_stats": [_p, _pi64],
     "qba_sample_check": [_p, C.c_int, _u64, _u64, _u64, _p, _u64, _p, _p, _p, C.c_int, _p],
+    "qba_sample_check_batched": [_p, C.c_int, _u64, _i64, _u64, _p, _u64, _u64, _p, _p, _p, _p],
     "qba_isq_indices": [_p, _p, _p, _u64, _p, _i64, _pi64, _p],
     "qba_select_eq": [_p, _p, _i64, _p, _i64, _p, _pi64, _p],
     "qba_gather": [_p, _p, _u64, _p, _i64, _p, _p],

@@ -164,81 +164,134 @@ __device__ __forceinline__ void qba_count_entry(const uint32_t (&row)[NP + 1], i
   }
 }
 
+// One thread-step: entries [c0, c0+4) of the launch (columns of `lists`).
 // MODE 0: sample -> lists;  MODE 1: sample -> lists + counts;  MODE 2: lists -> counts
+template <int NP, int MODE>
+__device__ __forceinline__ void qba_quad(uint64_t c0, uint64_t count, uint64_t first, uint32_t k0,
+                                         uint32_t k1, const QbaProgramSet *__restrict__ ps,
+                                         const uint64_t *pat, const uint64_t *apat,
+                                         const uint64_t *thr, uint8_t *__restrict__ lists,
+                                         uint64_t ld, uint32_t *hist) {
+  using C = QCfg<NP>;
+  using Out = typename C::Out;
+  const int valid = (count - c0) >= 4 ? 4 : (int)(count - c0);
+  uint32_t row[C::G];
+  if constexpr (MODE == 2) {
+    if (valid == 4) {
+#pragma unroll
+      for (int g = 0; g < C::G; ++g)
+        row[g] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(lists + g * ld + c0));
+    } else {
+#pragma unroll
+      for (int g = 0; g < C::G; ++g) {
+        row[g] = 0;
+        for (int j = 0; j < valid; ++j) row[g] |= (uint32_t)lists[g * ld + c0 + j] << (8 * j);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < C::G; ++g) row[g] = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < valid) {
+        const Out o = qba_sample_entry<NP>(first + c0 + j, k0, k1, ps, pat, apat, thr);
+#pragma unroll
+        for (int g = 0; g < C::G; ++g)
+          row[g] |= ((uint32_t)(o >> C::shift(g)) & (uint32_t)C::M) << (8 * j);
+      }
+    }
+    if (valid == 4) {
+#pragma unroll
+      for (int g = 0; g < C::G; ++g) *reinterpret_cast<uint32_t *>(lists + g * ld + c0) = row[g];
+    } else {
+#pragma unroll
+      for (int g = 0; g < C::G; ++g)
+        for (int j = 0; j < valid; ++j) lists[g * ld + c0 + j] = (uint8_t)(row[g] >> (8 * j));
+    }
+  }
+  if constexpr (MODE != 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < valid) qba_count_entry<NP>(row, j, hist);
+  }
+}
+
+// Stage the program's tables in LDS; returns the histogram base after them.
+template <int NP, int MODE>
+__device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__ ps, uint64_t *lds,
+                                               const uint64_t *&pat, const uint64_t *&apat,
+                                               const uint64_t *&thr) {
+  pat = apat = thr = lds;
+  uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
+  if constexpr (MODE != 2) {
+    const int T = ps->table_total;
+    const uint64_t *tab = reinterpret_cast<const uint64_t *>(ps + 1);
+    const int ntab = ps->any_nonuniform ? 3 * T : T;
+    for (int i = threadIdx.x; i < ntab; i += QBA_BLOCK) lds[i] = tab[i];
+    apat = lds + T;
+    thr = lds + 2 * T;
+    hist = reinterpret_cast<uint32_t *>(lds + ntab);
+  }
+  return hist;
+}
+
 template <int NP, int MODE>
 __global__ void __launch_bounds__(QBA_BLOCK)
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                 uint64_t count, uint8_t *__restrict__ lists, uint64_t ld,
                 uint32_t *__restrict__ slab) {
   using C = QCfg<NP>;
-  using Out = typename C::Out;
   extern __shared__ __align__(16) uint64_t lds[];
-  const int tid = threadIdx.x;
-  const uint64_t *pat = lds, *apat = lds, *thr = lds;
-  uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
-  if constexpr (MODE != 2) {
-    const int T = ps->table_total;
-    const uint64_t *tab = reinterpret_cast<const uint64_t *>(ps + 1);
-    const int ntab = ps->any_nonuniform ? 3 * T : T;
-    for (int i = tid; i < ntab; i += QBA_BLOCK) lds[i] = tab[i];
-    apat = lds + T;
-    thr = lds + 2 * T;
-    hist = reinterpret_cast<uint32_t *>(lds + ntab);
-  }
+  const uint64_t *pat, *apat, *thr;
+  uint32_t *hist = qba_stage<NP, MODE>(ps, lds, pat, apat, thr);
   if (MODE != 0)
-    for (int i = tid; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
+    for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
   __syncthreads();
-
   const uint64_t nquad = (count + 3) >> 2;
-  for (uint64_t q = (uint64_t)blockIdx.x * QBA_BLOCK + tid; q < nquad;
-       q += (uint64_t)gridDim.x * QBA_BLOCK) {
-    const uint64_t c0 = q << 2;
-    const int valid = (count - c0) >= 4 ? 4 : (int)(count - c0);
-    uint32_t row[C::G];
-    if constexpr (MODE == 2) {
-      if (valid == 4) {
-#pragma unroll
-        for (int g = 0; g < C::G; ++g)
-          row[g] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(lists + g * ld + c0));
-      } else {
-#pragma unroll
-        for (int g = 0; g < C::G; ++g) {
-          row[g] = 0;
-          for (int j = 0; j < valid; ++j) row[g] |= (uint32_t)lists[g * ld + c0 + j] << (8 * j);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < C::G; ++g) row[g] = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (j < valid) {
-          const Out o = qba_sample_entry<NP>(first + c0 + j, k0, k1, ps, pat, apat, thr);
-#pragma unroll
-          for (int g = 0; g < C::G; ++g)
-            row[g] |= ((uint32_t)(o >> C::shift(g)) & (uint32_t)C::M) << (8 * j);
-        }
-      }
-      if (valid == 4) {
-#pragma unroll
-        for (int g = 0; g < C::G; ++g)
-          *reinterpret_cast<uint32_t *>(lists + g * ld + c0) = row[g];
-      } else {
-#pragma unroll
-        for (int g = 0; g < C::G; ++g)
-          for (int j = 0; j < valid; ++j) lists[g * ld + c0 + j] = (uint8_t)(row[g] >> (8 * j));
-      }
-    }
-    if (MODE != 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (j < valid) qba_count_entry<NP>(row, j, hist);
-    }
-  }
+  for (uint64_t q = (uint64_t)blockIdx.x * QBA_BLOCK + threadIdx.x; q < nquad;
+       q += (uint64_t)gridDim.x * QBA_BLOCK)
+    qba_quad<NP, MODE>(q << 2, count, first, k0, k1, ps, pat, apat, thr, lists, ld, hist);
   if (MODE != 0) {
     __syncthreads();
     uint32_t *dst = slab + (size_t)blockIdx.x * C::NBINS;
-    for (int i = tid; i < C::NBINS; i += QBA_BLOCK) dst[i] = hist[i];
+    for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) dst[i] = hist[i];
+  }
+}
+
+// Batched independent instances (BASELINE configs[3]): instance i is its own
+// run with Philox key seed_base + i over entries [0, count).  A workgroup
+// owns whole instances, so its LDS histogram IS the instance's final count
+// and is written out directly (no slab, no reduce launch).
+template <int NP>
+__global__ void __launch_bounds__(QBA_BLOCK)
+    qba_k_batched(const QbaProgramSet *__restrict__ ps, uint64_t seed_base, int64_t n_inst,
+                  uint64_t count, uint8_t *__restrict__ lists, uint64_t ld, uint64_t inst_stride,
+                  int64_t *__restrict__ H, int64_t *__restrict__ Cc, int64_t *__restrict__ P) {
+  using C = QCfg<NP>;
+  extern __shared__ __align__(16) uint64_t lds[];
+  const uint64_t *pat, *apat, *thr;
+  uint32_t *hist = qba_stage<NP, 1>(ps, lds, pat, apat, thr);
+  const uint64_t nquad = (count + 3) >> 2;
+  for (int64_t inst = blockIdx.x; inst < n_inst; inst += gridDim.x) {
+    for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
+    __syncthreads();
+    const uint64_t key = seed_base + (uint64_t)inst;
+    uint8_t *L = lists + (uint64_t)inst * inst_stride;
+    for (uint64_t q = threadIdx.x; q < nquad; q += QBA_BLOCK)
+      qba_quad<NP, 1>(q << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps, pat, apat, thr,
+                      L, ld, hist);
+    __syncthreads();
+    int64_t *h = H + inst * C::HB, *c = Cc + inst * C::CB, *p = P + inst * C::W;
+    for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = hist[i];
+    for (int r = threadIdx.x; r < C::CB; r += QBA_BLOCK) {
+      const int u = r / (C::G * C::G), g = (r / C::G) % C::G, k = r % C::G;
+      const int64_t v = g < k ? hist[C::HB + r]
+                              : g > k ? hist[C::HB + (u * C::G + k) * C::G + g]
+                                      : hist[(u * C::G + 1) * C::W + u];
+      c[r] = v;
+    }
+    for (int u = threadIdx.x; u < C::W; u += QBA_BLOCK) p[u] = hist[(u * C::G + 1) * C::W + u];
+    __syncthreads();
   }
 }
 
@@ -351,20 +404,6 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
   return QBA_OK;
 }
 
-static int dispatch(qba_ctx *ctx, const QbaLaunch &L) {
-  switch (L.n) {
-#define QBA_CASE(k) \
-  case k:           \
-    return launch_np<k>(ctx, L);
-    QBA_CASE(1) QBA_CASE(2) QBA_CASE(3) QBA_CASE(4) QBA_CASE(5) QBA_CASE(6) QBA_CASE(7)
-    QBA_CASE(8) QBA_CASE(9) QBA_CASE(10) QBA_CASE(11) QBA_CASE(12) QBA_CASE(13) QBA_CASE(14)
-    QBA_CASE(15)
-#undef QBA_CASE
-    default:
-      return qba_fail(QBA_EUNSUPPORTED, "n_parties must be in [1, 15]");
-  }
-}
-
 static int check_common(qba_ctx *ctx, int n, const uint8_t *lists, uint64_t count, uint64_t ld,
                         const char *who) {
   if (!ctx) return qba_fail(QBA_EINVAL, std::string(who) + ": ctx is NULL");
@@ -383,6 +422,77 @@ static int need_program(qba_ctx *ctx, int n, const char *who) {
     return qba_fail(QBA_ESTATE, std::string(who) + ": no resource program compiled for n=" +
                                     std::to_string(n) + " (call qba_resource_compile for both kinds)");
   return QBA_OK;
+}
+
+struct QbaBatch {
+  int n;
+  const QbaProgramSet *ps;
+  uint64_t seed_base;
+  int64_t n_inst;
+  uint64_t count;
+  uint8_t *lists;
+  uint64_t ld, inst_stride;
+  int64_t *H, *C, *P;
+  hipStream_t stream;
+};
+
+template <int NP>
+static int launch_batched_np(qba_ctx *ctx, const QbaBatch &B) {
+  using C = QCfg<NP>;
+  const QbaProgramSet *hs = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP]);
+  size_t lds = (size_t)(hs->any_nonuniform ? 3 : 1) * hs->table_total * sizeof(uint64_t) +
+               (size_t)C::NBINS * sizeof(uint32_t);
+  lds = (lds + 15) & ~(size_t)15;
+  const int64_t cap = (int64_t)ctx->num_cus * 16;
+  const int grid = (int)(B.n_inst < cap ? B.n_inst : cap);
+  if (lds > 65536)
+    QBA_HIP(hipFuncSetAttribute((const void *)qba_k_batched<NP>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(qba_k_batched<NP>, dim3(grid), dim3(QBA_BLOCK), lds, B.stream, B.ps,
+                     B.seed_base, B.n_inst, B.count, B.lists, B.ld, B.inst_stride, B.H, B.C, B.P);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}
+
+extern "C" int qba_sample_check_batched(qba_ctx *ctx, int n, uint64_t seed_base, int64_t n_inst,
+                                        uint64_t count, uint8_t *lists, uint64_t ld,
+                                        uint64_t inst_stride, int64_t *H, int64_t *C, int64_t *P,
+                                        qba_stream stream) {
+  int rc = check_common(ctx, n, lists, count, ld, "qba_sample_check_batched");
+  if (rc) return rc;
+  if (n_inst < 0 || !H || !C || !P || (n_inst > 1 && inst_stride < (uint64_t)(n + 1) * ld) ||
+      (inst_stride & 3) || count >= (1ull << 31))
+    return qba_fail(QBA_EINVAL, "qba_sample_check_batched: bad arguments (inst_stride >= (n+1)*ld, "
+                                "multiple of 4; count < 2^31)");
+  if (n_inst == 0 || count == 0) return QBA_OK;
+  if ((rc = need_program(ctx, n, "qba_sample_check_batched"))) return rc;
+  QbaBatch B{n, (const QbaProgramSet *)ctx->prog_dev[n], seed_base, n_inst, count, lists, ld,
+             inst_stride, H, C, P, (hipStream_t)stream};
+  switch (n) {
+#define QBA_CASE(k) \
+  case k:           \
+    return launch_batched_np<k>(ctx, B);
+    QBA_CASE(1) QBA_CASE(2) QBA_CASE(3) QBA_CASE(4) QBA_CASE(5) QBA_CASE(6) QBA_CASE(7)
+    QBA_CASE(8) QBA_CASE(9) QBA_CASE(10) QBA_CASE(11) QBA_CASE(12) QBA_CASE(13) QBA_CASE(14)
+    QBA_CASE(15)
+#undef QBA_CASE
+    default:
+      return qba_fail(QBA_EUNSUPPORTED, "n_parties must be in [1, 15]");
+  }
+}
+
+static int dispatch(qba_ctx *ctx, const QbaLaunch &L) {
+  switch (L.n) {
+#define QBA_CASE(k) \
+  case k:           \
+    return launch_np<k>(ctx, L);
+    QBA_CASE(1) QBA_CASE(2) QBA_CASE(3) QBA_CASE(4) QBA_CASE(5) QBA_CASE(6) QBA_CASE(7)
+    QBA_CASE(8) QBA_CASE(9) QBA_CASE(10) QBA_CASE(11) QBA_CASE(12) QBA_CASE(13) QBA_CASE(14)
+    QBA_CASE(15)
+#undef QBA_CASE
+    default:
+      return qba_fail(QBA_EUNSUPPORTED, "n_parties must be in [1, 15]");
+  }
 }
 
 static int zero_counts(int n, int64_t *H, int64_t *C, int64_t *P, hipStream_t s) {

@@ -167,6 +167,24 @@ class Engine:
              _ptr(counts.H), _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
         return lists, counts
 
+    def sample_check_batched(self, n: int, seed_base: int, n_inst: int, count: int,
+                             lists: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Counts]:
+        """n_inst independent runs (key seed_base + i) of `count` entries each.
+        Returns lists [n_inst, n+1, ld] and per-instance counts [n_inst, ...]."""
+        self.prepare(n)
+        _, w = self.sizes(n)
+        ld = max(64, (count + 63) // 64 * 64)
+        if lists is None:
+            lists = torch.empty((n_inst, n + 1, ld), dtype=torch.uint8, device=self.device)
+        if lists.dim() != 3 or lists.shape[:2] != (n_inst, n + 1) or lists.stride(2) != 1:
+            raise QbaError("lists must be a uint8 [n_inst, n+1, ld] tensor")
+        z = lambda *s: torch.empty(s, dtype=torch.int64, device=self.device)  # noqa: E731
+        counts = Counts(z(n_inst, w, n + 1, w), z(n_inst, w, n + 1, n + 1), z(n_inst, w))
+        call("qba_sample_check_batched", self.ctx, n, seed_base, n_inst, count, _ptr(lists),
+             lists.stride(1), lists.stride(0), _ptr(counts.H), _ptr(counts.C), _ptr(counts.P),
+             self.stream())
+        return lists, counts
+
     # -- (A5-A8) count mode -------------------------------------------------------
     def check_counts(self, lists: torch.Tensor, n: int, count: int,
                      counts: Optional[Counts] = None, accumulate: bool = False) -> Counts:
