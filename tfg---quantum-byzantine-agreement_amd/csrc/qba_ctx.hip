@@ -44,7 +44,8 @@ extern "C" int qba_init(int device, qba_ctx **out) {
   ctx->device = device;
   ctx->num_cus = prop.multiProcessorCount;
   if (hipMalloc(&ctx->flag, 64) != hipSuccess || hipMalloc(&ctx->count1, 64) != hipSuccess ||
-      hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess) {
+      hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess ||
+      hipMalloc(&ctx->acc, 16 * 16 * 16 * 8 * 2 + 4096) != hipSuccess) {
     delete ctx;
     return qba_fail(QBA_ENOMEM, "qba_init: hipMalloc of flags failed");
   }
@@ -64,6 +65,7 @@ extern "C" int qba_destroy(qba_ctx *ctx) {
   if (ctx->flag) (void)hipFree(ctx->flag);
   if (ctx->count1) (void)hipFree(ctx->count1);
   if (ctx->stats) (void)hipFree(ctx->stats);
+  if (ctx->acc) (void)hipFree(ctx->acc);
   delete ctx;
   return QBA_OK;
 }

@@ -121,6 +121,7 @@ struct qba_ctx {
   int32_t *flag = nullptr;  // 1-word device flag
   int64_t *count1 = nullptr; // 1-word device counter
   int64_t *stats = nullptr;  // [2]: last counts launch: Q entries with a value >= w, spare
+  void *acc = nullptr;       // int64 column sums of the slab (max bins of any n)
 };
 
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes);

@@ -295,43 +295,56 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   }
 }
 
-// Sum the per-workgroup partials into the int64 outputs (see qba.h for shapes).
+// Column sums of the slab: workgroup (x, y) sums rows [y*R, (y+1)*R) of 256
+// bins and adds the partial into acc (integer atomics: order-independent, so
+// the result is bitwise reproducible).
 template <int NP>
 __global__ void __launch_bounds__(256)
-    qba_k_reduce(const uint32_t *__restrict__ slab, int nblocks, int64_t *__restrict__ H,
-                 int64_t *__restrict__ Cc, int64_t *__restrict__ P, int64_t *__restrict__ stats,
-                 int accumulate) {
+    qba_k_reduce_cols(const uint32_t *__restrict__ slab, int nblocks, int rows_per,
+                      unsigned long long *__restrict__ acc) {
+  using C = QCfg<NP>;
+  const int bin = blockIdx.x * 256 + threadIdx.x;
+  if (bin >= C::NBINS) return;
+  const int b0 = blockIdx.y * rows_per;
+  const int b1 = b0 + rows_per < nblocks ? b0 + rows_per : nblocks;
+  unsigned long long s = 0;
+  for (int b = b0; b < b1; ++b) s += slab[(size_t)b * C::NBINS + bin];
+  if (s) atomicAdd(&acc[bin], s);
+}
+
+// acc -> the int64 outputs (see qba.h for shapes): H as is, C symmetrised
+// with |P_u| on the diagonal, P[u] = |P_u| = H[u][1][u].
+template <int NP>
+__global__ void __launch_bounds__(256)
+    qba_k_finalize(const unsigned long long *__restrict__ acc, int64_t *__restrict__ H,
+                   int64_t *__restrict__ Cc, int64_t *__restrict__ P, int64_t *__restrict__ stats,
+                   int accumulate) {
   using C = QCfg<NP>;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  auto colsum = [&](int bin) {
-    int64_t s = 0;
-    for (int b = 0; b < nblocks; ++b) s += slab[(size_t)b * C::NBINS + bin];
-    return s;
-  };
   auto put = [&](int64_t *dst, int64_t v) { *dst = accumulate ? *dst + v : v; };
   if (i < C::HB) {
-    put(&H[i], colsum(i));
+    put(&H[i], (int64_t)acc[i]);
     return;
   }
   int r = i - C::HB;
   if (r < C::CB) {
     const int u = r / (C::G * C::G), g = (r / C::G) % C::G, h = r % C::G;
     if (g < h) {
-      const int64_t s = colsum(C::HB + r);
-      put(&Cc[r], s);
-      put(&Cc[(u * C::G + h) * C::G + g], s);
+      const int64_t v = (int64_t)acc[C::HB + r];
+      put(&Cc[r], v);
+      put(&Cc[(u * C::G + h) * C::G + g], v);
     } else if (g == h) {
-      put(&Cc[r], colsum((u * C::G + 1) * C::W + u));  // |P_u| = H[u][1][u]
+      put(&Cc[r], (int64_t)acc[(u * C::G + 1) * C::W + u]);
     }
     return;
   }
   r -= C::CB;
   if (r < C::W) {
-    put(&P[r], colsum((r * C::G + 1) * C::W + r));
+    put(&P[r], (int64_t)acc[(r * C::G + 1) * C::W + r]);
     return;
   }
   r -= C::W;
-  if (r < C::STATS && stats) stats[r] = colsum(C::HB + C::CB + r);
+  if (r < C::STATS && stats) stats[r] = (int64_t)acc[C::HB + C::CB + r];
 }
 
 // ---------------------------------------------------------------------------
@@ -397,9 +410,15 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
   int rc = L.mode == 0 ? go(qba_k_lists<NP, 0>) : L.mode == 1 ? go(qba_k_lists<NP, 1>)
                                                              : go(qba_k_lists<NP, 2>);
   if (rc || L.mode == 0) return rc;
+  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ctx->acc);
+  QBA_HIP(hipMemsetAsync(acc, 0, sizeof(unsigned long long) * C::NBINS, L.stream));
+  const int rows_per = 32;
+  hipLaunchKernelGGL(qba_k_reduce_cols<NP>, dim3((C::NBINS + 255) / 256, (grid + rows_per - 1) / rows_per),
+                     dim3(256), 0, L.stream, slab, grid, rows_per, acc);
+  QBA_HIP(hipGetLastError());
   const int items = C::HB + C::CB + C::W + C::STATS;
-  hipLaunchKernelGGL(qba_k_reduce<NP>, dim3((items + 255) / 256), dim3(256), 0, L.stream, slab,
-                     grid, L.H, L.C, L.P, L.stats, L.accumulate);
+  hipLaunchKernelGGL(qba_k_finalize<NP>, dim3((items + 255) / 256), dim3(256), 0, L.stream, acc,
+                     L.H, L.C, L.P, L.stats, L.accumulate);
   QBA_HIP(hipGetLastError());
   return QBA_OK;
 }
