@@ -45,7 +45,7 @@ extern "C" int qba_init(int device, qba_ctx **out) {
   ctx->num_cus = prop.multiProcessorCount;
   if (hipMalloc(&ctx->flag, 64) != hipSuccess || hipMalloc(&ctx->count1, 64) != hipSuccess ||
       hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess ||
-      hipMalloc(&ctx->acc, 16 * 16 * 16 * 8 * 2 + 4096) != hipSuccess) {
+      hipMalloc(&ctx->acc, (16 * 16 * 17 + 16 * 16 * 16 + 16) * 8) != hipSuccess) {
     delete ctx;
     return qba_fail(QBA_ENOMEM, "qba_init: hipMalloc of flags failed");
   }

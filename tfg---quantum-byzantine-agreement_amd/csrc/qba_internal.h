@@ -84,7 +84,10 @@ struct QbaProgramSet {
   int32_t table_total;
   int32_t any_nonuniform;
   int32_t n;
-  int32_t pad;
+  int32_t canonical;  // both programs have the standard layout of tfg.py's circuits:
+                      // not-Q = ceil(n*nQ/8) uniform byte factors over words x1.., tables
+                      // of 256 at f*256; Q = one uniform nQ-bit factor on x1.  The
+                      // sampler then takes its specialised path (qba_sample_entry_fast).
 };
 
 // ---------------------------------------------------------------------------

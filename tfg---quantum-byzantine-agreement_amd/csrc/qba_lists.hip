@@ -22,10 +22,16 @@ struct QCfg {
   static constexpr int NQ = (G <= 2) ? 1 : (G <= 4) ? 2 : (G <= 8) ? 3 : 4;
   static constexpr int N = G * NQ;  // qubits of the circuit (tfg.py:44)
   static constexpr int W = 1 << NQ;  // |W| (tfg.py:318)
-  static constexpr int HB = W * G * W;
+  static constexpr int HB = W * G * W;    // H as returned: [u][g][x]
+  static constexpr int WP = W + 1;        // LDS row stride of H: +1 word spreads banks
+  static constexpr int HBL = W * G * WP;  // H as counted in LDS / the slab
   static constexpr int CB = W * G * G;
   static constexpr int STATS = 2;  // [0] Q entries with a value >= W (invalid), [1] spare
-  static constexpr int NBINS = HB + CB + STATS;
+  static constexpr int NBINS = HBL + CB + STATS;
+  __host__ __device__ static constexpr int hidx(int u, int g, int x) { return (u * G + g) * WP + x; }
+  // number of not-Q table bytes of the canonical program (ceil(n*nQ/8))
+  static constexpr int NFB = (NP * NQ + 7) / 8;
+  static constexpr int LASTB = NP * NQ - 8 * (NFB - 1);
   using Out = typename std::conditional<(N <= 32), uint32_t, uint64_t>::type;
   static constexpr Out M = (Out)(W - 1);
   __host__ __device__ static constexpr int shift(int g) { return N - (g + 1) * NQ; }
@@ -128,6 +134,37 @@ __device__ __forceinline__ typename QCfg<NP>::Out qba_sample_entry(
   return out;
 }
 
+// Canonical programs (QbaProgramSet::canonical): every table column is a byte
+// of the stream, so the factor loop is fully unrolled at compile time.
+template <int NP>
+__device__ __forceinline__ typename QCfg<NP>::Out qba_sample_entry_fast(
+    uint64_t e, uint32_t k0, uint32_t k1, uint64_t perm_t, int qoff, const uint64_t *pat) {
+  using C = QCfg<NP>;
+  using Out = typename C::Out;
+  const uint32_t elo = (uint32_t)e, ehi = (uint32_t)(e >> 32);
+  const QbaU4 x = qba_philox(elo, ehi, 0u, 0u, k0, k1);
+  Out out;
+  if (x.x & 1u) {
+    Out mask;
+    bool ok = qba_perm<NP>((uint64_t)x.z | ((uint64_t)x.w << 32), perm_t, mask);
+    for (uint32_t a = 1; !ok; ++a) {
+      const QbaU4 y = qba_philox(elo, ehi, 0x80000000u + a, 0u, k0, k1);
+      ok = qba_perm<NP>((uint64_t)y.x | ((uint64_t)y.y << 32), perm_t, mask);
+    }
+    out = (Out)pat[qoff + (x.y & (uint32_t)C::M)] ^ mask;
+  } else {
+    out = 0;
+#pragma unroll
+    for (int f = 0; f < C::NFB; ++f) {
+      const uint32_t w = f < 4 ? x.y : (f < 8 ? x.z : x.w);
+      const uint32_t bits = f < C::NFB - 1 ? 8 : C::LASTB;
+      const uint32_t col = (w >> (8 * (f & 3))) & ((1u << bits) - 1u);
+      out ^= (Out)pat[256 * f + col];
+    }
+  }
+  return out;
+}
+
 // ---------------------------------------------------------------------------
 // count one entry (values are byte j of row[g])
 // ---------------------------------------------------------------------------
@@ -144,18 +181,18 @@ __device__ __forceinline__ void qba_count_entry(const uint32_t (&row)[NP + 1], i
   }
   if (l[0] == l[1]) return;  // not Q-correlated (tfg.py:327)
   if (any >= (uint32_t)C::W) {
-    atomicAdd(&hist[C::HB + C::CB + 0], 1u);
+    atomicAdd(&hist[C::HBL + C::CB + 0], 1u);
     return;
   }
-  uint32_t *h = hist + l[1] * (C::G * C::W);
+  uint32_t *h = hist + l[1] * (C::G * C::WP);
   uint32_t seen = 0;
 #pragma unroll
   for (int g = 0; g < C::G; ++g) {
-    atomicAdd(&h[g * C::W + l[g]], 1u);
+    atomicAdd(&h[g * C::WP + l[g]], 1u);
     seen |= 1u << l[g];
   }
   if (__popc(seen) != C::G) {  // some pair collides: exact slow path
-    uint32_t *c = hist + C::HB + l[1] * (C::G * C::G);
+    uint32_t *c = hist + C::HBL + l[1] * (C::G * C::G);
 #pragma unroll
     for (int g = 0; g < C::G; ++g)
 #pragma unroll
@@ -166,7 +203,7 @@ __device__ __forceinline__ void qba_count_entry(const uint32_t (&row)[NP + 1], i
 
 // One thread-step: entries [c0, c0+4) of the launch (columns of `lists`).
 // MODE 0: sample -> lists;  MODE 1: sample -> lists + counts;  MODE 2: lists -> counts
-template <int NP, int MODE>
+template <int NP, int MODE, bool FAST, bool TAIL>
 __device__ __forceinline__ void qba_quad(uint64_t c0, uint64_t count, uint64_t first, uint32_t k0,
                                          uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                          const uint64_t *pat, const uint64_t *apat,
@@ -174,7 +211,7 @@ __device__ __forceinline__ void qba_quad(uint64_t c0, uint64_t count, uint64_t f
                                          uint64_t ld, uint32_t *hist) {
   using C = QCfg<NP>;
   using Out = typename C::Out;
-  const int valid = (count - c0) >= 4 ? 4 : (int)(count - c0);
+  const int valid = !TAIL ? 4 : ((count - c0) >= 4 ? 4 : (int)(count - c0));
   uint32_t row[C::G];
   if constexpr (MODE == 2) {
     if (valid == 4) {
@@ -194,7 +231,12 @@ __device__ __forceinline__ void qba_quad(uint64_t c0, uint64_t count, uint64_t f
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j < valid) {
-        const Out o = qba_sample_entry<NP>(first + c0 + j, k0, k1, ps, pat, apat, thr);
+        Out o;
+        if constexpr (FAST)
+          o = qba_sample_entry_fast<NP>(first + c0 + j, k0, k1, ps->prog[1].perm_t,
+                                        ps->prog[0].table_len, pat);
+        else
+          o = qba_sample_entry<NP>(first + c0 + j, k0, k1, ps, pat, apat, thr);
 #pragma unroll
         for (int g = 0; g < C::G; ++g)
           row[g] |= ((uint32_t)(o >> C::shift(g)) & (uint32_t)C::M) << (8 * j);
@@ -235,7 +277,7 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   return hist;
 }
 
-template <int NP, int MODE>
+template <int NP, int MODE, bool FAST>
 __global__ void __launch_bounds__(QBA_BLOCK)
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                 uint64_t count, uint8_t *__restrict__ lists, uint64_t ld,
@@ -247,10 +289,13 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   if (MODE != 0)
     for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
   __syncthreads();
-  const uint64_t nquad = (count + 3) >> 2;
-  for (uint64_t q = (uint64_t)blockIdx.x * QBA_BLOCK + threadIdx.x; q < nquad;
+  const uint64_t nfull = count >> 2;
+  for (uint64_t q = (uint64_t)blockIdx.x * QBA_BLOCK + threadIdx.x; q < nfull;
        q += (uint64_t)gridDim.x * QBA_BLOCK)
-    qba_quad<NP, MODE>(q << 2, count, first, k0, k1, ps, pat, apat, thr, lists, ld, hist);
+    qba_quad<NP, MODE, FAST, false>(q << 2, count, first, k0, k1, ps, pat, apat, thr, lists, ld, hist);
+  if ((count & 3) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+    qba_quad<NP, MODE, false, true>(nfull << 2, count, first, k0, k1, ps, pat, apat, thr, lists, ld,
+                                    hist);
   if (MODE != 0) {
     __syncthreads();
     uint32_t *dst = slab + (size_t)blockIdx.x * C::NBINS;
@@ -262,7 +307,7 @@ __global__ void __launch_bounds__(QBA_BLOCK)
 // run with Philox key seed_base + i over entries [0, count).  A workgroup
 // owns whole instances, so its LDS histogram IS the instance's final count
 // and is written out directly (no slab, no reduce launch).
-template <int NP>
+template <int NP, bool FAST>
 __global__ void __launch_bounds__(QBA_BLOCK)
     qba_k_batched(const QbaProgramSet *__restrict__ ps, uint64_t seed_base, int64_t n_inst,
                   uint64_t count, uint8_t *__restrict__ lists, uint64_t ld, uint64_t inst_stride,
@@ -271,26 +316,29 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   extern __shared__ __align__(16) uint64_t lds[];
   const uint64_t *pat, *apat, *thr;
   uint32_t *hist = qba_stage<NP, 1>(ps, lds, pat, apat, thr);
-  const uint64_t nquad = (count + 3) >> 2;
   for (int64_t inst = blockIdx.x; inst < n_inst; inst += gridDim.x) {
     for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
     __syncthreads();
     const uint64_t key = seed_base + (uint64_t)inst;
     uint8_t *L = lists + (uint64_t)inst * inst_stride;
-    for (uint64_t q = threadIdx.x; q < nquad; q += QBA_BLOCK)
-      qba_quad<NP, 1>(q << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps, pat, apat, thr,
-                      L, ld, hist);
+    const uint64_t nfull = count >> 2;
+    for (uint64_t q = threadIdx.x; q < nfull; q += QBA_BLOCK)
+      qba_quad<NP, 1, FAST, false>(q << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps, pat,
+                                   apat, thr, L, ld, hist);
+    if ((count & 3) && threadIdx.x == 0)
+      qba_quad<NP, 1, false, true>(nfull << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps,
+                                   pat, apat, thr, L, ld, hist);
     __syncthreads();
     int64_t *h = H + inst * C::HB, *c = Cc + inst * C::CB, *p = P + inst * C::W;
-    for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = hist[i];
+    for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = hist[(i / C::W) * C::WP + i % C::W];
     for (int r = threadIdx.x; r < C::CB; r += QBA_BLOCK) {
       const int u = r / (C::G * C::G), g = (r / C::G) % C::G, k = r % C::G;
-      const int64_t v = g < k ? hist[C::HB + r]
-                              : g > k ? hist[C::HB + (u * C::G + k) * C::G + g]
-                                      : hist[(u * C::G + 1) * C::W + u];
+      const int64_t v = g < k ? hist[C::HBL + r]
+                              : g > k ? hist[C::HBL + (u * C::G + k) * C::G + g]
+                                      : hist[C::hidx(u, 1, u)];
       c[r] = v;
     }
-    for (int u = threadIdx.x; u < C::W; u += QBA_BLOCK) p[u] = hist[(u * C::G + 1) * C::W + u];
+    for (int u = threadIdx.x; u < C::W; u += QBA_BLOCK) p[u] = hist[C::hidx(u, 1, u)];
     __syncthreads();
   }
 }
@@ -323,28 +371,28 @@ __global__ void __launch_bounds__(256)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   auto put = [&](int64_t *dst, int64_t v) { *dst = accumulate ? *dst + v : v; };
   if (i < C::HB) {
-    put(&H[i], (int64_t)acc[i]);
+    put(&H[i], (int64_t)acc[(i / C::W) * C::WP + i % C::W]);
     return;
   }
   int r = i - C::HB;
   if (r < C::CB) {
     const int u = r / (C::G * C::G), g = (r / C::G) % C::G, h = r % C::G;
     if (g < h) {
-      const int64_t v = (int64_t)acc[C::HB + r];
+      const int64_t v = (int64_t)acc[C::HBL + r];
       put(&Cc[r], v);
       put(&Cc[(u * C::G + h) * C::G + g], v);
     } else if (g == h) {
-      put(&Cc[r], (int64_t)acc[(u * C::G + 1) * C::W + u]);
+      put(&Cc[r], (int64_t)acc[C::hidx(u, 1, u)]);
     }
     return;
   }
   r -= C::CB;
   if (r < C::W) {
-    put(&P[r], (int64_t)acc[(r * C::G + 1) * C::W + r]);
+    put(&P[r], (int64_t)acc[C::hidx(r, 1, r)]);
     return;
   }
   r -= C::W;
-  if (r < C::STATS && stats) stats[r] = (int64_t)acc[C::HB + C::CB + r];
+  if (r < C::STATS && stats) stats[r] = (int64_t)acc[C::HBL + C::CB + r];
 }
 
 // ---------------------------------------------------------------------------
@@ -364,7 +412,7 @@ struct QbaLaunch {
 
 static int nbins_of(int n) {
   const int g = n + 1, q = qba_nq(n), w = 1 << q;
-  return w * g * w + w * g * g + 2;
+  return w * g * (w + 1) + w * g * g + 2;
 }
 
 static int grid_for(qba_ctx *ctx, int mode, uint64_t count) {
@@ -407,8 +455,11 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
     QBA_HIP(hipGetLastError());
     return QBA_OK;
   };
-  int rc = L.mode == 0 ? go(qba_k_lists<NP, 0>) : L.mode == 1 ? go(qba_k_lists<NP, 1>)
-                                                             : go(qba_k_lists<NP, 2>);
+  const bool fast = L.mode != 2 &&
+                    reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP])->canonical;
+  int rc = L.mode == 2 ? go(qba_k_lists<NP, 2, false>)
+           : fast      ? (L.mode == 0 ? go(qba_k_lists<NP, 0, true>) : go(qba_k_lists<NP, 1, true>))
+                       : (L.mode == 0 ? go(qba_k_lists<NP, 0, false>) : go(qba_k_lists<NP, 1, false>));
   if (rc || L.mode == 0) return rc;
   unsigned long long *acc = reinterpret_cast<unsigned long long *>(ctx->acc);
   QBA_HIP(hipMemsetAsync(acc, 0, sizeof(unsigned long long) * C::NBINS, L.stream));
@@ -464,11 +515,12 @@ static int launch_batched_np(qba_ctx *ctx, const QbaBatch &B) {
   lds = (lds + 15) & ~(size_t)15;
   const int64_t cap = (int64_t)ctx->num_cus * 16;
   const int grid = (int)(B.n_inst < cap ? B.n_inst : cap);
+  auto kern = hs->canonical ? qba_k_batched<NP, true> : qba_k_batched<NP, false>;
   if (lds > 65536)
-    QBA_HIP(hipFuncSetAttribute((const void *)qba_k_batched<NP>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(qba_k_batched<NP>, dim3(grid), dim3(QBA_BLOCK), lds, B.stream, B.ps,
-                     B.seed_base, B.n_inst, B.count, B.lists, B.ld, B.inst_stride, B.H, B.C, B.P);
+    QBA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(QBA_BLOCK), lds, B.stream, B.ps, B.seed_base,
+                     B.n_inst, B.count, B.lists, B.ld, B.inst_stride, B.H, B.C, B.P);
   QBA_HIP(hipGetLastError());
   return QBA_OK;
 }

@@ -293,6 +293,23 @@ extern "C" int qba_resource_compile(qba_ctx *ctx, int n, int kind, const int32_t
     ps->table_total = T;
     ps->any_nonuniform = a.p.any_nonuniform | b.p.any_nonuniform;
     ps->n = n;
+    ps->canonical = 1;
+    {
+      const int nbits = n * nq, nf = (nbits + 7) / 8;
+      const QbaProgram &pa = ps->prog[0], &pb = ps->prog[1];
+      if (pa.nfac != nf || pb.nfac != 1 || ps->any_nonuniform) ps->canonical = 0;
+      for (int f = 0; f < pa.nfac && ps->canonical; ++f) {
+        const QbaFactor &F = pa.fac[f];
+        const int want_bits = f < nf - 1 ? 8 : nbits - 8 * (nf - 1);
+        if (F.bits != want_bits || !F.uniform || F.offset != 256 * f || F.col_word != f / 4 ||
+            F.col_shift != 8 * (f % 4))
+          ps->canonical = 0;
+      }
+      const QbaFactor &Q = pb.fac[0];
+      if (Q.bits != nq || !Q.uniform || Q.col_word != 0 || Q.col_shift != 0 ||
+          Q.offset != a.p.table_len || a.p.table_len != 256 * (nf - 1) + (1 << (nbits - 8 * (nf - 1))))
+        ps->canonical = 0;
+    }
     uint64_t *tab = reinterpret_cast<uint64_t *>(ps + 1);
     std::copy(a.pat.begin(), a.pat.end(), tab);
     std::copy(b.pat.begin(), b.pat.end(), tab + a.pat.size());

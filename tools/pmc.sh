@@ -3,6 +3,7 @@
 # MI355X guide prescribes).  Usage: tools/pmc.sh <outdir> <bench args...>
 set -e
 out=$1; shift
+mkdir -p "${GRAFT_REPO_ROOT:-.}/$out"
 root=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd /tmp && export TMPDIR=/tmp
 i=0
