@@ -58,11 +58,11 @@ def cpu_baseline(n, seed, info, target_s):
     import oracle_lib
     sample = 1 << 18
     t0 = time.perf_counter()
-    oracle_lib.sample_counts(n, seed, 0, sample, info["notq"], info["q"])
+    oracle_lib.sample_counts(n, seed, 0, sample, info["notq"], info["q"], info["closed"])
     dt = time.perf_counter() - t0
     sample = int(min(max(sample, sample * target_s / max(dt, 1e-6)), 1 << 27))
     t0 = time.perf_counter()
-    oracle_lib.sample_counts(n, seed, 0, sample, info["notq"], info["q"])
+    oracle_lib.sample_counts(n, seed, 0, sample, info["notq"], info["q"], info["closed"])
     dt = time.perf_counter() - t0
     return {"value": sample / dt, "unit": "entries/s", "cores": oracle_lib.threads(), "kind": "port",
             "sample": f"{sample} entries of the same n={n} workload: C twin (oracle/sampler_ref.c) "

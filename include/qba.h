@@ -99,6 +99,18 @@ QBA_API int qba_program_export(qba_ctx *ctx, int n_parties, int kind, int32_t *n
                        uint64_t *apat_host, uint64_t *thr_host, int32_t table_cap,
                        int32_t *table_len);
 
+/* Sampler selection of the compiled pair (synchronous, host only):
+ * flags[0] = canonical table layout, flags[1] = closed form (n <= 11 and both
+ * programs proven equal to tfg.py's circuits' distributions), flags[2] =
+ * 2^32 mod n!, flags[3..5] = permutation stage sizes A, B, C. */
+QBA_API int qba_program_flags(qba_ctx *ctx, int n_parties, int32_t *flags_host /* [6] */);
+
+/* Host only (no device needed): the closed-form permutation stage tables for
+ * n in [1, 11] (layout in csrc/qba_internal.h).  sizes[0..5] = RA, RB, RC,
+ * word offset of B, word offset of C, total words; `words` may be NULL to
+ * query the size. */
+QBA_API int qba_perm_tables(int n_parties, uint32_t *words_host, int32_t cap, int32_t *sizes_host /* [6] */);
+
 /* ---- (A3/A4) Born sampling: Philox4x32-10 keyed by the GLOBAL entry index -------- */
 /* Replaces generacionListas (tfg.py:68-84) + measure_to_ints (tfg.py:128-129):
  * writes lists[g][k - first] for entries k in [first, first+count). */

@@ -49,11 +49,15 @@ def _prog_args(prog: dict):
     return keep, [C.c_int(int(prog["nfac"])), _p(desc), _p(pat), _p(apat), _p(thr)]
 
 
-def sample(n: int, seed: int, first: int, count: int, prog_notq: dict, prog_q: dict) -> np.ndarray:
+def sample(n: int, seed: int, first: int, count: int, prog_notq: dict, prog_q: dict,
+           closed: bool = False) -> np.ndarray:
+    """Lists of entries [first, first+count); `closed` selects the closed-form
+    schedule the engine uses when its program flags say so (n <= 11)."""
     lists = np.zeros((n + 1, max(count, 1)), np.uint8)
     k0, a0 = _prog_args(prog_notq)
     k1, a1 = _prog_args(prog_q)
-    lib().oracle_sample(C.c_int(n), C.c_uint64(seed), C.c_uint64(first), C.c_uint64(count), *a0, *a1,
+    lib().oracle_sample(C.c_int(n), C.c_uint64(seed), C.c_uint64(first), C.c_uint64(count),
+                        C.c_int(int(closed)), *a0, *a1,
                         _p(lists), C.c_uint64(lists.shape[1]))
     return lists[:, :count]
 
@@ -69,7 +73,8 @@ def counts(lists: np.ndarray, n: int):
     return H, Cc, P, int(bad)
 
 
-def sample_counts(n: int, seed: int, first: int, count: int, prog_notq: dict, prog_q: dict):
+def sample_counts(n: int, seed: int, first: int, count: int, prog_notq: dict, prog_q: dict,
+                  closed: bool = False):
     lists = np.zeros((n + 1, max(count, 1)), np.uint8)
     w = 1 << n_qubits(n)
     H = np.zeros((w, n + 1, w), np.int64)
@@ -78,7 +83,7 @@ def sample_counts(n: int, seed: int, first: int, count: int, prog_notq: dict, pr
     k0, a0 = _prog_args(prog_notq)
     k1, a1 = _prog_args(prog_q)
     lib().oracle_sample_counts(C.c_int(n), C.c_uint64(seed), C.c_uint64(first), C.c_uint64(count),
-                               *a0, *a1, _p(lists), C.c_uint64(lists.shape[1]), _p(H), _p(Cc), _p(P))
+                               C.c_int(int(closed)), *a0, *a1, _p(lists), C.c_uint64(lists.shape[1]), _p(H), _p(Cc), _p(P))
     return lists[:, :count], H, Cc, P
 
 

@@ -154,18 +154,83 @@ static uint64_t sample_outcome(int n, uint64_t seed, uint64_t e, const prog_t *n
   return draw_program(&r, 1, q) ^ mask;
 }
 
+/* Closed-form schedule (csrc/qba_lists.hip, "Closed-form sampler"), used by
+ * the engine for n <= 11 when both programs are proven to be tfg.py's
+ * circuits' distributions.  Restated here from its definition: the rank
+ * R = floor(F * n! / 2^32) is decoded directly into forward Fisher-Yates
+ * digits (the engine instead splits it into three table indices). */
+static void closed_entry(int n, uint64_t seed, uint64_t e, uint8_t vals[16]) {
+  const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  const uint32_t ctr[4] = {(uint32_t)e, (uint32_t)(e >> 32), 0u, 0u};
+  uint32_t x[4];
+  philox4x32_10(ctr, key, x);
+  const int nq = n_qubits(n);
+  const uint32_t W = 1u << nq;
+  if (!(x[0] & 1u)) { /* not-Q: L0 = L1, L1..Ln independent uniform */
+    uint32_t v[16];
+    for (int b = 0; b < 4; ++b) {
+      v[b] = (x[1] >> (8 * b)) & (W - 1);
+      v[4 + b] = (x[1] >> (8 * b + 4)) & (W - 1);
+      v[8 + b] = (x[2] >> (8 * b)) & (W - 1);
+      v[12 + b] = (x[2] >> (8 * b + 4)) & (W - 1);
+    }
+    vals[0] = (uint8_t)v[0];
+    for (int g = 1; g <= n; ++g) vals[g] = (uint8_t)v[g - 1];
+    return;
+  }
+  uint32_t nfact = 1;
+  for (int i = 2; i <= n; ++i) nfact *= (uint32_t)i;
+  const uint32_t t = (uint32_t)((1ull << 32) % nfact);
+  uint32_t cand[4] = {x[2], x[3], 0, 0};
+  int nc = 2, ci = 0;
+  uint32_t a = 0, F = 0;
+  for (;;) {
+    if (ci == nc) {
+      const uint32_t c2[4] = {(uint32_t)e, (uint32_t)(e >> 32), 0x80000000u + ++a, 0u};
+      philox4x32_10(c2, key, cand);
+      nc = 4;
+      ci = 0;
+    }
+    F = cand[ci++];
+    if ((uint32_t)(F * nfact) >= t) break;
+  }
+  uint32_t R = (uint32_t)(((uint64_t)F * nfact) >> 32);
+  int perm[16];
+  for (int p = 0; p < 16; ++p) perm[p] = p;
+  uint32_t div = nfact;
+  for (int i = 1; i < n; ++i) { /* digit of position i has radix n - i + 1 */
+    div /= (uint32_t)(n - i + 1);
+    const int d = (int)(R / div);
+    R %= div;
+    const int j = i + d, tmp = perm[i];
+    perm[i] = perm[j];
+    perm[j] = tmp;
+  }
+  const uint32_t r = (x[0] >> 1) & (W - 1);
+  for (int g = 0; g <= n; ++g) vals[g] = (uint8_t)(r ^ (uint32_t)perm[g]);
+}
+
 static void outcome_to_column(uint64_t out, int n, uint8_t *lists, uint64_t ld, uint64_t col) {
   const int nq = n_qubits(n), N = (n + 1) * nq;
   for (int g = 0; g <= n; ++g)
     lists[(uint64_t)g * ld + col] = (uint8_t)((out >> (N - (g + 1) * nq)) & ((1u << nq) - 1u));
 }
 
-void oracle_sample(int n, uint64_t seed, uint64_t first, uint64_t count, int nfac0,
+void oracle_sample(int n, uint64_t seed, uint64_t first, uint64_t count, int closed, int nfac0,
                    const int32_t *desc0, const uint64_t *pat0, const uint64_t *apat0,
                    const uint64_t *thr0, int nfac1, const int32_t *desc1, const uint64_t *pat1,
                    const uint64_t *apat1, const uint64_t *thr1, uint8_t *lists, uint64_t ld) {
   const prog_t p0 = {nfac0, desc0, pat0, apat0, thr0}, p1 = {nfac1, desc1, pat1, apat1, thr1};
   const uint64_t t = perm_threshold(n);
+  if (closed) {
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < (int64_t)count; ++k) {
+      uint8_t vals[16];
+      closed_entry(n, seed, first + (uint64_t)k, vals);
+      for (int g = 0; g <= n; ++g) lists[(uint64_t)g * ld + (uint64_t)k] = vals[g];
+    }
+    return;
+  }
 #pragma omp parallel for schedule(static)
   for (int64_t k = 0; k < (int64_t)count; ++k)
     outcome_to_column(sample_outcome(n, seed, first + (uint64_t)k, &p0, &p1, t), n, lists, ld,
@@ -233,12 +298,12 @@ int64_t oracle_counts(int n, const uint8_t *lists, uint64_t count, uint64_t ld, 
 
 /* Fused CPU baseline: sample every entry and count it, writing the lists once
  * (the same work as one qba_sample_check step).  Returns invalid entries. */
-int64_t oracle_sample_counts(int n, uint64_t seed, uint64_t first, uint64_t count, int nfac0,
+int64_t oracle_sample_counts(int n, uint64_t seed, uint64_t first, uint64_t count, int closed, int nfac0,
                              const int32_t *desc0, const uint64_t *pat0, const uint64_t *apat0,
                              const uint64_t *thr0, int nfac1, const int32_t *desc1,
                              const uint64_t *pat1, const uint64_t *apat1, const uint64_t *thr1,
                              uint8_t *lists, uint64_t ld, int64_t *H, int64_t *Cc, int64_t *P) {
-  oracle_sample(n, seed, first, count, nfac0, desc0, pat0, apat0, thr0, nfac1, desc1, pat1, apat1,
+  oracle_sample(n, seed, first, count, closed, nfac0, desc0, pat0, apat0, thr0, nfac1, desc1, pat1, apat1,
                 thr1, lists, ld);
   return oracle_counts(n, lists, count, ld, H, Cc, P);
 }

@@ -1,0 +1,126 @@
+"""Closed-form sampler (n <= 11): host-built permutation stage tables and the
+oracle's restatement of the schedule.  CPU only (no device calls).
+
+The engine draws pi by forward Fisher-Yates over positions 1..n whose digit
+string is the mixed-radix rank R = floor(F * n! / 2^32); R is split into three
+table indices (A: positions 1..3 when n >= 8; B, C: the 8-byte window holding
+the rest, composed with v_perm_b32).  These tests restate that composition in
+Python and check it against the direct Fisher-Yates decode of every rank
+(n <= 8) or of 20k ranks (n = 9..11).
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from conftest import sub
+
+
+def fy_decode(n, R):
+    """Forward Fisher-Yates: digit of position i has radix n-i+1, first most significant."""
+    perm = list(range(16))
+    div = math.factorial(n)
+    for i in range(1, n):
+        div //= n - i + 1
+        d, R = divmod(R, div)
+        perm[i], perm[i + d] = perm[i + d], perm[i]
+    return perm[: n + 1]
+
+
+def tables(n):
+    lib = sub("_lib")
+    sizes = np.zeros(6, np.int32)
+    lib.call("qba_perm_tables", n, None, 0, sizes.ctypes.data_as(lib._pi32))
+    words = np.zeros(int(sizes[5]), np.uint32)
+    lib.call("qba_perm_tables", n, words.ctypes.data, len(words), sizes.ctypes.data_as(lib._pi32))
+    return sizes, words
+
+
+def vperm(hi, lo, sel):
+    """v_perm_b32 restricted to selector bytes 0..7 (byte b of {hi:lo})."""
+    src = [(lo >> (8 * b)) & 0xFF for b in range(4)] + [(hi >> (8 * b)) & 0xFF for b in range(4)]
+    return sum(src[(sel >> (8 * b)) & 0xFF] << (8 * b) for b in range(4))
+
+
+def compose(n, sizes, words, R):
+    ra, rb, rc, offb, offc, _ = (int(x) for x in sizes)
+    iA, rest = divmod(R, rb * rc)
+    iB, iC = divmod(rest, rc)
+    q = [int(w) for w in words[4 * iA: 4 * iA + 4]]
+    win = 1 if n >= 8 else 0
+    w0, w1 = q[win], q[win + 1]
+    sb = words[offb + 2 * iB: offb + 2 * iB + 2]
+    y0, y1 = vperm(w1, w0, int(sb[0])), vperm(w1, w0, int(sb[1]))
+    sc = words[offc + 2 * iC: offc + 2 * iC + 2]
+    q[win], q[win + 1] = vperm(y1, y0, int(sc[0])), vperm(y1, y0, int(sc[1]))
+    return [(q[g // 4] >> (8 * (g % 4))) & 0xFF for g in range(n + 1)]
+
+
+@pytest.mark.parametrize("n", list(range(1, 12)))
+def test_stage_tables_compose_to_fisher_yates(n):
+    sizes, words = tables(n)
+    ra, rb, rc = (int(x) for x in sizes[:3])
+    assert ra * rb * rc == math.factorial(n)
+    assert ra == (n * (n - 1) * (n - 2) if n >= 8 else 1)
+    nf = math.factorial(n)
+    ranks = range(nf) if nf <= 40320 else \
+        [0, nf - 1] + list(np.random.default_rng(n).integers(0, nf, 20_000))
+    for R in ranks:
+        assert compose(n, sizes, words, int(R)) == fy_decode(n, int(R)), (n, R)
+
+
+def closed_entry_py(n, seed, e):
+    """Python restatement of the closed-form schedule for one entry."""
+    nq = oracle_lib.n_qubits(n)
+    W = 1 << nq
+    x = [int(v) for v in oracle_lib.philox(np.array([e & 0xFFFFFFFF, e >> 32, 0, 0], np.uint32), seed)[0]]
+    if not x[0] & 1:
+        vals = [(x[1] >> (8 * b)) & (W - 1) for b in range(4)] + \
+               [(x[1] >> (8 * b + 4)) & (W - 1) for b in range(4)] + \
+               [(x[2] >> (8 * b)) & (W - 1) for b in range(4)] + \
+               [(x[2] >> (8 * b + 4)) & (W - 1) for b in range(4)]
+        return [vals[0]] + vals[: n]
+    nf = math.factorial(n)
+    t = (1 << 32) % nf
+    cands, a = [x[2], x[3]], 0
+    while True:
+        if not cands:
+            a += 1
+            cands = [int(v) for v in oracle_lib.philox(
+                np.array([e & 0xFFFFFFFF, e >> 32, 0x80000000 + a, 0], np.uint32), seed)[0]]
+        F = cands.pop(0)
+        if (F * nf) & 0xFFFFFFFF >= t:
+            break
+    perm = fy_decode(n, (F * nf) >> 32)
+    r = (x[0] >> 1) & (W - 1)
+    return [r ^ p for p in perm]
+
+
+@pytest.mark.parametrize("n", [1, 3, 7, 8, 11])
+def test_oracle_closed_schedule(n):
+    seed, first, count = 0xC0FFEE ^ n, (1 << 35) + 11, 300
+    info = {"nfac": 0, "desc": np.zeros((0, 6), np.int32), "pat": np.zeros(1, np.uint64),
+            "apat": np.zeros(1, np.uint64), "thr": np.zeros(1, np.uint64)}
+    got = oracle_lib.sample(n, seed, first, count, info, info, closed=True)
+    for k in range(count):
+        assert list(got[:, k]) == closed_entry_py(n, seed, first + k), k
+
+
+def test_oracle_closed_statistics():
+    """n = 11: Q entries are r ^ pi (all distinct), not-Q entries have L0 == L1,
+    marginals uniform."""
+    n, count = 11, 200_000
+    info = {"nfac": 0, "desc": np.zeros((0, 6), np.int32), "pat": np.zeros(1, np.uint64),
+            "apat": np.zeros(1, np.uint64), "thr": np.zeros(1, np.uint64)}
+    L = oracle_lib.sample(n, 99, 0, count, info, info, closed=True).astype(np.int64)
+    q = L[0] != L[1]
+    assert abs(q.mean() - 0.5) < 0.01
+    srt = np.sort(L[:, q], axis=0)
+    assert (np.diff(srt, axis=0) > 0).all()
+    perm = L[:, q] ^ L[0, q]
+    assert (np.sort(perm[1:], axis=0) == np.arange(1, n + 1)[:, None]).all()
+    for g in range(n + 1):
+        cnt = np.bincount(L[g], minlength=16)
+        chi2 = ((cnt - count / 16) ** 2 / (count / 16)).sum()
+        assert chi2 < 60, (g, chi2)

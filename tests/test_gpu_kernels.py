@@ -107,7 +107,7 @@ def test_sampler_bit_exact(engine, n, first, count):
     lists = engine.sample(n, seed, first, count)
     torch.cuda.synchronize()
     got = lists[:, :count].cpu().numpy()
-    ref = oracle_lib.sample(n, seed, first, count, info["notq"], info["q"])
+    ref = oracle_lib.sample(n, seed, first, count, info["notq"], info["q"], info["closed"])
     assert np.array_equal(got, ref)
 
 
@@ -152,7 +152,7 @@ def test_counts_match_oracle(engine, n, count):
     lists, c_fused = engine.sample_check(n, seed, 5, count)
     c_sep = engine.check_counts(lists, n, count)
     torch.cuda.synchronize()
-    ref_lists = oracle_lib.sample(n, seed, 5, count, info["notq"], info["q"])
+    ref_lists = oracle_lib.sample(n, seed, 5, count, info["notq"], info["q"], info["closed"])
     H, C, P, bad = oracle_lib.counts(ref_lists, n)
     assert bad == 0
     for c in (c_fused, c_sep):
@@ -295,9 +295,50 @@ def test_batched_instances(engine):
     lists, c = engine.sample_check_batched(n, base, n_inst, count)
     torch.cuda.synchronize()
     for i in (0, 1, 17, 36):
-        ref = oracle_lib.sample(n, base + i, 0, count, info["notq"], info["q"])
+        ref = oracle_lib.sample(n, base + i, 0, count, info["notq"], info["q"], info["closed"])
         assert np.array_equal(lists[i, :, :count].cpu().numpy(), ref)
         H, C, P, bad = oracle_lib.counts(ref, n)
         assert np.array_equal(c.H[i].cpu().numpy(), H)
         assert np.array_equal(c.C[i].cpu().numpy(), C)
         assert np.array_equal(c.P[i].cpu().numpy(), P)
+
+
+def test_closed_form_flags(engine):
+    """tfg.py's two circuits compile to the closed-form sampler for n <= 11
+    (the programs are proven to be exactly their distributions) and to the
+    canonical-table sampler above."""
+    for n in (1, 2, 3, 7, 8, 11, 12, 15):
+        info = engine.prepare(n)
+        assert info["canonical"]
+        assert info["closed"] == (n <= 11), n
+
+
+def test_general_program_path(engine):
+    """A circuit pair that is NOT tfg.py's (group 3 = copy of group 2 in the
+    not-Q circuit) runs on the general alias-table sampler; bit-exact vs the
+    C twin, and the count pass on its lists matches the oracle."""
+    resource = sub("resource")
+    n = 3
+    nq = resource.n_qubits(n)
+    notq = resource.Gate((n + 1) * nq)
+    for qb in range(nq, 3 * nq):
+        notq.add_operation("H", targets=qb)
+    for j in range(nq):
+        notq.add_operation("X", targets=j, controls=nq + j)
+        notq.add_operation("X", targets=3 * nq + j, controls=2 * nq + j)
+    q = resource.qCorrelated(n, nq, perm=[1, 2, 3])
+    try:
+        info = engine.compile(n, notq, q)
+        assert not info["closed"] and not info["canonical"]
+        seed, count = 4242, 70_001
+        lists, counts = engine.sample_check(n, seed, 3, count)
+        torch.cuda.synchronize()
+        got = lists[:, :count].cpu().numpy()
+        ref = oracle_lib.sample(n, seed, 3, count, info["notq"], info["q"], False)
+        assert np.array_equal(got, ref)
+        assert np.array_equal(got[3][got[0] == got[1]], got[2][got[0] == got[1]])
+        H, C, P, bad = oracle_lib.counts(ref, n)
+        gH, gC, gP = counts.numpy()
+        assert bad == 0 and np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+    finally:
+        engine.prepare(n, perm=list(range(1, n + 1)))

@@ -36,6 +36,8 @@ SIGNATURES = {
     "qba_sv_support": [_p, _p, C.c_int, _f64, _p, _p, _i64, _pi64, _p],
     "qba_resource_compile": [_p, C.c_int, C.c_int, _pi32, C.c_int, _pi32],
     "qba_program_export": [_p, C.c_int, C.c_int, _pi32, _pi32, _pu64, _pu64, _pu64, _i32, _pi32],
+    "qba_program_flags": [_p, C.c_int, _pi32],
+    "qba_perm_tables": [C.c_int, _p, _i32, _pi32],
     "qba_sample": [_p, C.c_int, _u64, _u64, _u64, _p, _u64, _p],
     "qba_check_counts": [_p, C.c_int, _p, _u64, _u64, _p, _p, _p, C.c_int, _p],
     "qba_last_stats": [_p, _pi64],

@@ -88,7 +88,25 @@ struct QbaProgramSet {
                       // not-Q = ceil(n*nQ/8) uniform byte factors over words x1.., tables
                       // of 256 at f*256; Q = one uniform nQ-bit factor on x1.  The
                       // sampler then takes its specialised path (qba_sample_entry_fast).
+  // Closed-form sampler (n <= 11 and the programs proven to be exactly the
+  // distributions of tfg.py's two circuits, see qba_resource.hip):
+  //   not-Q: L0 = L1, L1..Ln independent uniform;  Q: L_g = r ^ pi(g).
+  // pi is drawn by forward Fisher-Yates over positions 1..n whose mixed-radix
+  // digit string is split into three table indices (stage A: positions 1..3
+  // when n >= 8; stages B, C: the 8-byte window that holds the rest) and
+  // composed with v_perm_b32.  Random-bit schedule in qba_lists.hip.
+  int32_t closed;
+  uint32_t t32;             // 2^32 mod n!  (Lemire rejection threshold, 32-bit)
+  uint32_t nfact;           // n!
+  uint32_t ra, rb, rc;      // stage sizes, ra * rb * rc = n!
+  int32_t perm_off;         // byte offset of the stage tables from the image start
+  int32_t perm_words;       // u32 words of stage tables: A [ra][4], B [rb][2], C [rc][2]
 };
+
+// Closed-form stage tables (host-built, staged to LDS): 4 + 2 + 2 words per
+// entry of A, B, C.  Largest: n = 11 -> 990*4 + 1680*2 + 24*2 = 7368 words.
+#define QBA_PERM_MAX_WORDS 7400
+#define QBA_CLOSED_MAX_N 11
 
 // ---------------------------------------------------------------------------
 // error reporting / context

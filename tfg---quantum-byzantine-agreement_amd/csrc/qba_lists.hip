@@ -166,106 +166,291 @@ __device__ __forceinline__ typename QCfg<NP>::Out qba_sample_entry_fast(
 }
 
 // ---------------------------------------------------------------------------
-// count one entry (values are byte j of row[g])
+// Closed-form sampler (QbaProgramSet::closed; n <= 11).  Per entry e:
+//   x = philox(ctr = {e_lo, e_hi, 0, 0}, key = seed);  isQ = x0 & 1
+//   not-Q: values v_0..v_15 = the nQ low bits of the bytes of x1, x1 >> 4,
+//          x2, x2 >> 4 (in that order); group g >= 1 takes v_{g-1}, group 0
+//          takes v_0 (= group 1, tfg.py:15-22).
+//   Q:     r = (x0 >> 1) & (W-1); the rank F is the first of x2, x3 whose
+//          F * n! mod 2^32 >= 2^32 mod n! (Lemire: exactly uniform); if both
+//          fail, the words of philox(ctr = {e_lo, e_hi, 0x80000000 + a, 0})
+//          for a = 1, 2, ... in order.  (iA, iB, iC) = the mixed-radix digits
+//          of floor(F * n! / 2^32) in radices (RA, RB, RC) [F * RA = iA:F1,
+//          F1 * RB = iB:F2, F2 * RC = iC:F3], pi = stage A[iA] with its window
+//          permuted by B[iB] then C[iC]; group g = r ^ pi(g) (tfg.py:25-40).
+// Values are produced as bytes, group g in byte g % 4 of word g / 4.
 // ---------------------------------------------------------------------------
 template <int NP>
-__device__ __forceinline__ void qba_count_entry(const uint32_t (&row)[NP + 1], int j,
-                                                uint32_t *hist) {
+struct CF {
   using C = QCfg<NP>;
-  uint32_t l[C::G];
-  uint32_t any = 0;
-#pragma unroll
-  for (int g = 0; g < C::G; ++g) {
-    l[g] = (row[g] >> (8 * j)) & 0xffu;
-    any |= l[g];
+  static constexpr int G = NP + 1;
+  static constexpr int ND = (G + 3) / 4;          // words per entry
+  static constexpr int WIN = NP >= 8 ? 1 : 0;      // first word of the 8-byte window
+  static constexpr int K = NP >= 8 ? NP - 3 : NP;  // window positions that move
+  static constexpr uint32_t fact(int a, int b) {   // a * (a-1) * ... * b
+    uint32_t x = 1;
+    for (int i = a; i >= b; --i) x *= (uint32_t)i;
+    return x;
   }
-  if (l[0] == l[1]) return;  // not Q-correlated (tfg.py:327)
-  if (any >= (uint32_t)C::W) {
+  static constexpr uint32_t RA = NP >= 8 ? fact(NP, NP - 2) : 1u;
+  static constexpr uint32_t RB = K >= 2 ? fact(K, (K - 3 > 2 ? K - 3 : 2)) : 1u;
+  static constexpr uint32_t RC = K >= 6 ? fact(K - 4, 2) : 1u;
+  static constexpr uint32_t NFACT = fact(NP, 2);
+  static constexpr uint32_t T32 = (uint32_t)((1ull << 32) % NFACT);
+  static constexpr int OFFB = 4 * (int)RA;            // in words
+  static constexpr int OFFC = OFFB + 2 * (int)RB;
+  static constexpr int WORDS = OFFC + 2 * (int)RC;
+  static constexpr uint32_t M4 = (uint32_t)(C::W - 1) * 0x01010101u;
+};
+
+__device__ __forceinline__ uint32_t qba_perm_b(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// first acceptable rank word among a, b (Lemire test); ok = 0 if neither
+template <int NP>
+__device__ __forceinline__ uint32_t qba_pick2(uint32_t a, uint32_t b, bool &ok) {
+  using F = CF<NP>;
+  const bool oa = a * F::NFACT >= F::T32, ob = b * F::NFACT >= F::T32;
+  ok = oa || ob;
+  return oa ? a : b;
+}
+
+template <int NP>
+__device__ __forceinline__ void qba_closed_entry(uint64_t e, uint32_t k0, uint32_t k1,
+                                                 const uint32_t *__restrict__ pl,
+                                                 uint32_t (&D)[CF<NP>::ND]) {
+  using F = CF<NP>;
+  const uint32_t elo = (uint32_t)e, ehi = (uint32_t)(e >> 32);
+  const QbaU4 x = qba_philox(elo, ehi, 0u, 0u, k0, k1);
+  // not-Q words
+  uint32_t nq[4];
+  {
+    const uint32_t a = x.y & F::M4, b = (x.y >> 4) & F::M4, c = x.z & F::M4, d = (x.z >> 4) & F::M4;
+    nq[0] = qba_perm_b(a, a, 0x02010000u);
+    nq[1] = qba_perm_b(b, a, 0x06050403u);
+    nq[2] = qba_perm_b(c, b, 0x06050403u);
+    nq[3] = qba_perm_b(d, c, 0x06050403u);
+  }
+  // Q words
+  bool ok;
+  uint32_t rank = qba_pick2<NP>(x.z, x.w, ok);
+  if (__builtin_expect(!ok, 0)) {  // probability (T32 / 2^32)^2 per Q entry
+    for (uint32_t a = 1; !ok; ++a) {
+      const QbaU4 y = qba_philox(elo, ehi, 0x80000000u + a, 0u, k0, k1);
+      bool o1, o2;
+      const uint32_t r1 = qba_pick2<NP>(y.x, y.y, o1), r2 = qba_pick2<NP>(y.z, y.w, o2);
+      ok = o1 || o2;
+      rank = o1 ? r1 : r2;
+    }
+  }
+  uint32_t iA = 0, rem = rank;
+  if constexpr (F::RA > 1) {
+    const uint64_t p = (uint64_t)rem * F::RA;
+    iA = (uint32_t)(p >> 32);
+    rem = (uint32_t)p;
+  }
+  const uint64_t pb = (uint64_t)rem * F::RB;
+  const uint32_t iB = (uint32_t)(pb >> 32);
+  const uint4 A = *reinterpret_cast<const uint4 *>(pl + 4 * iA);
+  const uint2 sB = *reinterpret_cast<const uint2 *>(pl + F::OFFB + 2 * iB);
+  uint32_t q[4] = {A.x, A.y, A.z, A.w};
+  uint32_t w0 = q[F::WIN], w1 = q[F::WIN + 1];
+  uint32_t y0 = qba_perm_b(w1, w0, sB.x), y1 = qba_perm_b(w1, w0, sB.y);
+  if constexpr (F::RC > 1) {
+    const uint32_t iC = (uint32_t)(((uint64_t)(uint32_t)pb * F::RC) >> 32);
+    const uint2 sC = *reinterpret_cast<const uint2 *>(pl + F::OFFC + 2 * iC);
+    const uint32_t z0 = qba_perm_b(y1, y0, sC.x), z1 = qba_perm_b(y1, y0, sC.y);
+    y0 = z0;
+    y1 = z1;
+  }
+  q[F::WIN] = y0;
+  q[F::WIN + 1] = y1;
+  const uint32_t R = ((x.x >> 1) & (uint32_t)(QCfg<NP>::W - 1)) * 0x01010101u;
+  const bool isq = x.x & 1u;
+#pragma unroll
+  for (int i = 0; i < F::ND; ++i) D[i] = isq ? (q[i] ^ R) : nq[i];
+}
+
+// Outcome word of the table samplers -> byte layout.
+template <int NP>
+__device__ __forceinline__ void qba_out_to_d(typename QCfg<NP>::Out o, uint32_t (&D)[CF<NP>::ND]) {
+  using C = QCfg<NP>;
+#pragma unroll
+  for (int i = 0; i < CF<NP>::ND; ++i) D[i] = 0;
+#pragma unroll
+  for (int g = 0; g < C::G; ++g)
+    D[g / 4] |= ((uint32_t)(o >> C::shift(g)) & (uint32_t)C::M) << (8 * (g % 4));
+}
+
+// 4x4 byte transpose: r_i byte j = input j byte i (an involution).
+__device__ __forceinline__ void qba_t4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t &r0,
+                                       uint32_t &r1, uint32_t &r2, uint32_t &r3) {
+  const uint32_t t0 = qba_perm_b(b, a, 0x06020400u), t1 = qba_perm_b(b, a, 0x07030501u);
+  const uint32_t t2 = qba_perm_b(d, c, 0x06020400u), t3 = qba_perm_b(d, c, 0x07030501u);
+  r0 = qba_perm_b(t2, t0, 0x05040100u);
+  r1 = qba_perm_b(t3, t1, 0x05040100u);
+  r2 = qba_perm_b(t2, t0, 0x07060302u);
+  r3 = qba_perm_b(t3, t1, 0x07060302u);
+}
+
+// v_pk_lshlrev_b16: each 16-bit half of `one` shifted by the low 4 bits of
+// the same half of `amt` (the upper bits of the half are ignored by the ALU).
+__device__ __forceinline__ uint32_t qba_pk_onehot(uint32_t amt, uint32_t one) {
+  uint32_t r;
+  asm("v_pk_lshlrev_b16 %0, %1, %2" : "=v"(r) : "v"(amt), "v"(one));
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// count one entry (group g = byte g % 4 of D[g / 4])
+//   Q-correlated iff L0 != L1 (tfg.py:327); u = L1 (tfg.py:182);
+//   H[u][g][L_g] += 1 for every g; C[u][g][h] += 1 for every equal pair --
+//   the pair loop runs only when the entry's distinct-value count (union of
+//   16-bit one-hots) is below n+1.
+// ---------------------------------------------------------------------------
+template <int NP>
+__device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uint32_t one,
+                                            uint32_t *hist) {
+  using C = QCfg<NP>;
+  using F = CF<NP>;
+  const uint32_t l0 = D[0] & 0xffu, l1 = (D[0] >> 8) & 0xffu;
+  if (l0 == l1) return;
+  uint32_t bad = 0;
+#pragma unroll
+  for (int i = 0; i < F::ND; ++i) {
+    uint32_t vm = 0;  // bits that must be clear: value bits >= W of the real groups
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (4 * i + b < C::G) vm |= (0xffu & ~(uint32_t)(C::W - 1)) << (8 * b);
+    bad |= D[i] & vm;
+  }
+  if (bad) {
     atomicAdd(&hist[C::HBL + C::CB + 0], 1u);
     return;
   }
-  uint32_t *h = hist + l[1] * (C::G * C::WP);
-  uint32_t seen = 0;
+  char *hb = reinterpret_cast<char *>(hist) + l1 * (uint32_t)(C::G * C::WP * 4);
 #pragma unroll
-  for (int g = 0; g < C::G; ++g) {
-    atomicAdd(&h[g * C::WP + l[g]], 1u);
-    seen |= 1u << l[g];
+  for (int i = 0; i < F::ND; ++i) {
+    const uint32_t E = D[i] << 2;  // byte b = 4 * value (< 64: no carry into the next byte)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int g = 4 * i + b;
+      if (g < C::G) atomicAdd(reinterpret_cast<uint32_t *>(hb + ((E >> (8 * b)) & 0xffu)) + g * C::WP, 1u);
+    }
   }
-  if (__popc(seen) != C::G) {  // some pair collides: exact slow path
-    uint32_t *c = hist + C::HBL + l[1] * (C::G * C::G);
+  uint32_t U = 0;
 #pragma unroll
+  for (int i = 0; i < F::ND; ++i) {
+    uint32_t mp = 0, mq = 0;
+    if (4 * i + 0 < C::G) mp |= 0x0000ffffu;
+    if (4 * i + 2 < C::G) mp |= 0xffff0000u;
+    if (4 * i + 1 < C::G) mq |= 0x0000ffffu;
+    if (4 * i + 3 < C::G) mq |= 0xffff0000u;
+    U |= (qba_pk_onehot(D[i], one) & mp) | (qba_pk_onehot(D[i] >> 8, one) & mq);
+  }
+  U = (U | (U >> 16)) & 0xffffu;
+  if (__popc(U) != C::G) {  // some pair collides: exact slow path
+    uint32_t l[C::G];
+#pragma unroll
+    for (int g = 0; g < C::G; ++g) l[g] = (D[g / 4] >> (8 * (g % 4))) & 0xffu;
+    uint32_t *c = hist + C::HBL + l1 * (C::G * C::G);
     for (int g = 0; g < C::G; ++g)
-#pragma unroll
       for (int k = g + 1; k < C::G; ++k)
         if (l[g] == l[k]) atomicAdd(&c[g * C::G + k], 1u);
   }
 }
 
+// Samplers of one entry into the byte layout
+enum { QBA_S_GENERAL = 0, QBA_S_FAST = 1, QBA_S_CLOSED = 2 };
+
+template <int NP, int SAMP>
+__device__ __forceinline__ void qba_entry_d(uint64_t e, uint32_t k0, uint32_t k1,
+                                            const QbaProgramSet *__restrict__ ps,
+                                            const uint64_t *pat, const uint64_t *apat,
+                                            const uint64_t *thr, const uint32_t *pl,
+                                            uint32_t (&D)[CF<NP>::ND]) {
+  if constexpr (SAMP == QBA_S_CLOSED) {
+    qba_closed_entry<NP>(e, k0, k1, pl, D);
+  } else if constexpr (SAMP == QBA_S_FAST) {
+    qba_out_to_d<NP>(qba_sample_entry_fast<NP>(e, k0, k1, ps->prog[1].perm_t, ps->prog[0].table_len, pat), D);
+  } else {
+    qba_out_to_d<NP>(qba_sample_entry<NP>(e, k0, k1, ps, pat, apat, thr), D);
+  }
+}
+
 // One thread-step: entries [c0, c0+4) of the launch (columns of `lists`).
 // MODE 0: sample -> lists;  MODE 1: sample -> lists + counts;  MODE 2: lists -> counts
-template <int NP, int MODE, bool FAST, bool TAIL>
+template <int NP, int MODE, int SAMP, bool TAIL>
 __device__ __forceinline__ void qba_quad(uint64_t c0, uint64_t count, uint64_t first, uint32_t k0,
                                          uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                          const uint64_t *pat, const uint64_t *apat,
-                                         const uint64_t *thr, uint8_t *__restrict__ lists,
-                                         uint64_t ld, uint32_t *hist) {
+                                         const uint64_t *thr, const uint32_t *pl,
+                                         uint8_t *__restrict__ lists, uint64_t ld, uint32_t *hist) {
   using C = QCfg<NP>;
-  using Out = typename C::Out;
+  constexpr int ND = CF<NP>::ND;
   const int valid = !TAIL ? 4 : ((count - c0) >= 4 ? 4 : (int)(count - c0));
-  uint32_t row[C::G];
+  uint32_t D[4][ND];
+  uint32_t row[4 * ND];
   if constexpr (MODE == 2) {
+#pragma unroll
+    for (int g = 0; g < 4 * ND; ++g) row[g] = 0;
     if (valid == 4) {
 #pragma unroll
       for (int g = 0; g < C::G; ++g)
         row[g] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(lists + g * ld + c0));
     } else {
-#pragma unroll
-      for (int g = 0; g < C::G; ++g) {
-        row[g] = 0;
+      for (int g = 0; g < C::G; ++g)
         for (int j = 0; j < valid; ++j) row[g] |= (uint32_t)lists[g * ld + c0 + j] << (8 * j);
-      }
     }
-  } else {
 #pragma unroll
-    for (int g = 0; g < C::G; ++g) row[g] = 0;
+    for (int i = 0; i < ND; ++i)
+      qba_t4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3], D[0][i], D[1][i], D[2][i],
+             D[3][i]);
+  } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j < valid) {
-        Out o;
-        if constexpr (FAST)
-          o = qba_sample_entry_fast<NP>(first + c0 + j, k0, k1, ps->prog[1].perm_t,
-                                        ps->prog[0].table_len, pat);
-        else
-          o = qba_sample_entry<NP>(first + c0 + j, k0, k1, ps, pat, apat, thr);
+        qba_entry_d<NP, SAMP>(first + c0 + j, k0, k1, ps, pat, apat, thr, pl, D[j]);
+      } else {
 #pragma unroll
-        for (int g = 0; g < C::G; ++g)
-          row[g] |= ((uint32_t)(o >> C::shift(g)) & (uint32_t)C::M) << (8 * j);
+        for (int i = 0; i < ND; ++i) D[j][i] = 0;
       }
     }
+#pragma unroll
+    for (int i = 0; i < ND; ++i)
+      qba_t4(D[0][i], D[1][i], D[2][i], D[3][i], row[4 * i], row[4 * i + 1], row[4 * i + 2],
+             row[4 * i + 3]);
     if (valid == 4) {
 #pragma unroll
       for (int g = 0; g < C::G; ++g) *reinterpret_cast<uint32_t *>(lists + g * ld + c0) = row[g];
     } else {
-#pragma unroll
       for (int g = 0; g < C::G; ++g)
         for (int j = 0; j < valid; ++j) lists[g * ld + c0 + j] = (uint8_t)(row[g] >> (8 * j));
     }
   }
   if constexpr (MODE != 0) {
+    const uint32_t one = 0x00010001u;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (j < valid) qba_count_entry<NP>(row, j, hist);
+      if (j < valid) qba_count_d<NP>(D[j], one, hist);
   }
 }
 
 // Stage the program's tables in LDS; returns the histogram base after them.
-template <int NP, int MODE>
+template <int NP, int MODE, int SAMP>
 __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__ ps, uint64_t *lds,
                                                const uint64_t *&pat, const uint64_t *&apat,
-                                               const uint64_t *&thr) {
+                                               const uint64_t *&thr, const uint32_t *&pl) {
   pat = apat = thr = lds;
+  pl = reinterpret_cast<const uint32_t *>(lds);
   uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
-  if constexpr (MODE != 2) {
+  if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
+    for (int i = threadIdx.x; i < CF<NP>::WORDS; i += QBA_BLOCK) dst[i] = src[i];
+    hist = dst + ((CF<NP>::WORDS + 3) & ~3);
+  } else if constexpr (MODE != 2) {
     const int T = ps->table_total;
     const uint64_t *tab = reinterpret_cast<const uint64_t *>(ps + 1);
     const int ntab = ps->any_nonuniform ? 3 * T : T;
@@ -277,7 +462,7 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   return hist;
 }
 
-template <int NP, int MODE, bool FAST>
+template <int NP, int MODE, int SAMP>
 __global__ void __launch_bounds__(QBA_BLOCK)
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                 uint64_t count, uint8_t *__restrict__ lists, uint64_t ld,
@@ -285,17 +470,18 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   using C = QCfg<NP>;
   extern __shared__ __align__(16) uint64_t lds[];
   const uint64_t *pat, *apat, *thr;
-  uint32_t *hist = qba_stage<NP, MODE>(ps, lds, pat, apat, thr);
+  const uint32_t *pl;
+  uint32_t *hist = qba_stage<NP, MODE, SAMP>(ps, lds, pat, apat, thr, pl);
   if (MODE != 0)
     for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
   __syncthreads();
   const uint64_t nfull = count >> 2;
   for (uint64_t q = (uint64_t)blockIdx.x * QBA_BLOCK + threadIdx.x; q < nfull;
        q += (uint64_t)gridDim.x * QBA_BLOCK)
-    qba_quad<NP, MODE, FAST, false>(q << 2, count, first, k0, k1, ps, pat, apat, thr, lists, ld, hist);
+    qba_quad<NP, MODE, SAMP, false>(q << 2, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
   if ((count & 3) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
-    qba_quad<NP, MODE, false, true>(nfull << 2, count, first, k0, k1, ps, pat, apat, thr, lists, ld,
-                                    hist);
+    qba_quad<NP, MODE, SAMP, true>(nfull << 2, count, first, k0, k1, ps, pat, apat, thr, pl, lists,
+                                   ld, hist);
   if (MODE != 0) {
     __syncthreads();
     uint32_t *dst = slab + (size_t)blockIdx.x * C::NBINS;
@@ -307,7 +493,7 @@ __global__ void __launch_bounds__(QBA_BLOCK)
 // run with Philox key seed_base + i over entries [0, count).  A workgroup
 // owns whole instances, so its LDS histogram IS the instance's final count
 // and is written out directly (no slab, no reduce launch).
-template <int NP, bool FAST>
+template <int NP, int SAMP>
 __global__ void __launch_bounds__(QBA_BLOCK)
     qba_k_batched(const QbaProgramSet *__restrict__ ps, uint64_t seed_base, int64_t n_inst,
                   uint64_t count, uint8_t *__restrict__ lists, uint64_t ld, uint64_t inst_stride,
@@ -315,7 +501,8 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   using C = QCfg<NP>;
   extern __shared__ __align__(16) uint64_t lds[];
   const uint64_t *pat, *apat, *thr;
-  uint32_t *hist = qba_stage<NP, 1>(ps, lds, pat, apat, thr);
+  const uint32_t *pl;
+  uint32_t *hist = qba_stage<NP, 1, SAMP>(ps, lds, pat, apat, thr, pl);
   for (int64_t inst = blockIdx.x; inst < n_inst; inst += gridDim.x) {
     for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
     __syncthreads();
@@ -323,11 +510,11 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     uint8_t *L = lists + (uint64_t)inst * inst_stride;
     const uint64_t nfull = count >> 2;
     for (uint64_t q = threadIdx.x; q < nfull; q += QBA_BLOCK)
-      qba_quad<NP, 1, FAST, false>(q << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps, pat,
-                                   apat, thr, L, ld, hist);
+      qba_quad<NP, 1, SAMP, false>(q << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps, pat,
+                                   apat, thr, pl, L, ld, hist);
     if ((count & 3) && threadIdx.x == 0)
-      qba_quad<NP, 1, false, true>(nfull << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps,
-                                   pat, apat, thr, L, ld, hist);
+      qba_quad<NP, 1, SAMP, true>(nfull << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps,
+                                  pat, apat, thr, pl, L, ld, hist);
     __syncthreads();
     int64_t *h = H + inst * C::HB, *c = Cc + inst * C::CB, *p = P + inst * C::W;
     for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = hist[(i / C::W) * C::WP + i % C::W];
@@ -428,14 +615,40 @@ static int grid_for(qba_ctx *ctx, int mode, uint64_t count) {
   return (int)g;
 }
 
+// Sampler of the compiled pair: closed form when proven (n <= 11), else the
+// canonical-table fast path, else the general alias-table path.
+template <int NP>
+static int sampler_of(const QbaProgramSet *hs) {
+  if (NP <= QBA_CLOSED_MAX_N && hs->closed) return QBA_S_CLOSED;
+  return hs->canonical ? QBA_S_FAST : QBA_S_GENERAL;
+}
+
+// LDS bytes of the staged tables for a sampling launch
+template <int NP>
+static size_t table_lds(const QbaProgramSet *hs, int samp) {
+  if (samp == QBA_S_CLOSED) return (size_t)((CF<NP>::WORDS + 3) & ~3) * sizeof(uint32_t);
+  return (size_t)(hs->any_nonuniform ? 3 : 1) * hs->table_total * sizeof(uint64_t);
+}
+
+template <int NP>
+static int check_closed(const QbaProgramSet *hs) {
+  if (hs->closed && (hs->ra != CF<NP>::RA || hs->rb != CF<NP>::RB || hs->rc != CF<NP>::RC ||
+                     hs->perm_words != CF<NP>::WORDS || hs->t32 != CF<NP>::T32))
+    return qba_fail(QBA_EINVAL, "closed-form program does not match the kernel's stage layout");
+  return QBA_OK;
+}
+
 template <int NP>
 static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
   using C = QCfg<NP>;
   const int grid = grid_for(ctx, L.mode, L.count);
+  const QbaProgramSet *hs = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP]);
+  int samp = QBA_S_GENERAL;
   size_t lds = 0;
   if (L.mode != 2) {
-    const QbaProgramSet *hs = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP]);
-    lds += (size_t)(hs->any_nonuniform ? 3 : 1) * hs->table_total * sizeof(uint64_t);
+    samp = sampler_of<NP>(hs);
+    if (int rc = check_closed<NP>(hs)) return rc;
+    lds += table_lds<NP>(hs, samp);
   }
   if (L.mode != 0) lds += (size_t)C::NBINS * sizeof(uint32_t);
   lds = (lds + 15) & ~(size_t)15;
@@ -455,11 +668,19 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
     QBA_HIP(hipGetLastError());
     return QBA_OK;
   };
-  const bool fast = L.mode != 2 &&
-                    reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP])->canonical;
-  int rc = L.mode == 2 ? go(qba_k_lists<NP, 2, false>)
-           : fast      ? (L.mode == 0 ? go(qba_k_lists<NP, 0, true>) : go(qba_k_lists<NP, 1, true>))
-                       : (L.mode == 0 ? go(qba_k_lists<NP, 0, false>) : go(qba_k_lists<NP, 1, false>));
+  int rc;
+  if (L.mode == 2) {
+    rc = go(qba_k_lists<NP, 2, QBA_S_GENERAL>);
+  } else if (samp == QBA_S_CLOSED) {
+    if constexpr (NP <= QBA_CLOSED_MAX_N)
+      rc = L.mode == 0 ? go(qba_k_lists<NP, 0, QBA_S_CLOSED>) : go(qba_k_lists<NP, 1, QBA_S_CLOSED>);
+    else
+      rc = qba_fail(QBA_EUNSUPPORTED, "closed form beyond n = 11");
+  } else if (samp == QBA_S_FAST) {
+    rc = L.mode == 0 ? go(qba_k_lists<NP, 0, QBA_S_FAST>) : go(qba_k_lists<NP, 1, QBA_S_FAST>);
+  } else {
+    rc = L.mode == 0 ? go(qba_k_lists<NP, 0, QBA_S_GENERAL>) : go(qba_k_lists<NP, 1, QBA_S_GENERAL>);
+  }
   if (rc || L.mode == 0) return rc;
   unsigned long long *acc = reinterpret_cast<unsigned long long *>(ctx->acc);
   QBA_HIP(hipMemsetAsync(acc, 0, sizeof(unsigned long long) * C::NBINS, L.stream));
@@ -510,19 +731,26 @@ template <int NP>
 static int launch_batched_np(qba_ctx *ctx, const QbaBatch &B) {
   using C = QCfg<NP>;
   const QbaProgramSet *hs = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP]);
-  size_t lds = (size_t)(hs->any_nonuniform ? 3 : 1) * hs->table_total * sizeof(uint64_t) +
-               (size_t)C::NBINS * sizeof(uint32_t);
+  const int samp = sampler_of<NP>(hs);
+  if (int rc = check_closed<NP>(hs)) return rc;
+  size_t lds = table_lds<NP>(hs, samp) + (size_t)C::NBINS * sizeof(uint32_t);
   lds = (lds + 15) & ~(size_t)15;
   const int64_t cap = (int64_t)ctx->num_cus * 16;
   const int grid = (int)(B.n_inst < cap ? B.n_inst : cap);
-  auto kern = hs->canonical ? qba_k_batched<NP, true> : qba_k_batched<NP, false>;
-  if (lds > 65536)
-    QBA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(QBA_BLOCK), lds, B.stream, B.ps, B.seed_base,
-                     B.n_inst, B.count, B.lists, B.ld, B.inst_stride, B.H, B.C, B.P);
-  QBA_HIP(hipGetLastError());
-  return QBA_OK;
+  auto go = [&](auto kern) -> int {
+    if (lds > 65536)
+      QBA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(QBA_BLOCK), lds, B.stream, B.ps, B.seed_base,
+                       B.n_inst, B.count, B.lists, B.ld, B.inst_stride, B.H, B.C, B.P);
+    QBA_HIP(hipGetLastError());
+    return QBA_OK;
+  };
+  if (samp == QBA_S_CLOSED) {
+    if constexpr (NP <= QBA_CLOSED_MAX_N) return go(qba_k_batched<NP, QBA_S_CLOSED>);
+    return qba_fail(QBA_EUNSUPPORTED, "closed form beyond n = 11");
+  }
+  return samp == QBA_S_FAST ? go(qba_k_batched<NP, QBA_S_FAST>) : go(qba_k_batched<NP, QBA_S_GENERAL>);
 }
 
 extern "C" int qba_sample_check_batched(qba_ctx *ctx, int n, uint64_t seed_base, int64_t n_inst,

@@ -141,6 +141,122 @@ static uint64_t factorial(int n) {
   return f;
 }
 
+
+// ---------------------------------------------------------------------------
+// Closed form.  The not-Q program is exactly "L0 = L1, L1..Ln independent
+// uniform" iff (i) every factor is uniform with distinct patterns, (ii) the
+// factors touch disjoint bits, (iii) in every pattern the bits of field 0 equal
+// those of field 1 and (iv) the factors carry n*nQ bits in all: the choices
+// then map one-to-one onto the W^n words with field0 == field1.  The Q program
+// (permutation mask removed) is the GHZ register iff it is one uniform factor
+// whose patterns are exactly {r in every field : r < W}.
+// ---------------------------------------------------------------------------
+static bool notq_closed(const QbaHostProgram &hp, int n) {
+  const int nq = qba_nq(n), N = (n + 1) * nq;
+  uint64_t seen_mask = 0;
+  int bits = 0;
+  for (int f = 0; f < hp.p.nfac; ++f) {
+    const QbaFactor &F = hp.p.fac[f];
+    if (!F.uniform) return false;
+    const int K = 1 << F.bits;
+    std::vector<uint64_t> pats(hp.pat.begin() + F.offset, hp.pat.begin() + F.offset + K);
+    uint64_t m = 0;
+    for (uint64_t p : pats) {
+      m |= p;
+      for (int j = 0; j < nq; ++j) {
+        const int b0 = N - 1 - j, b1 = N - 1 - (nq + j);  // qubit j of field 0 / field 1
+        if (((p >> b0) & 1) != ((p >> b1) & 1)) return false;
+      }
+    }
+    std::sort(pats.begin(), pats.end());
+    if (std::adjacent_find(pats.begin(), pats.end()) != pats.end()) return false;
+    if (m & seen_mask) return false;
+    seen_mask |= m;
+    bits += F.bits;
+  }
+  return bits == n * nq;
+}
+
+static bool q_closed(const QbaHostProgram &hp, int n) {
+  const int nq = qba_nq(n), N = (n + 1) * nq, W = 1 << nq;
+  if (hp.p.nfac != 1 || !hp.p.fac[0].uniform || hp.p.fac[0].bits != nq) return false;
+  std::vector<uint64_t> got(hp.pat.begin() + hp.p.fac[0].offset,
+                            hp.pat.begin() + hp.p.fac[0].offset + W), want;
+  for (int r = 0; r < W; ++r) {
+    uint64_t p = 0;
+    for (int g = 0; g <= n; ++g) p |= (uint64_t)r << (N - (g + 1) * nq);
+    want.push_back(p);
+  }
+  std::sort(got.begin(), got.end());
+  return got == want;
+}
+
+// Stage tables of the closed-form permutation (forward Fisher-Yates over
+// positions 1..n, digit d_i in [0, n-i+1) swaps positions i and i+d_i).
+//   A (n >= 8): digits of positions 1..3 -> the whole 12-byte array after
+//      those swaps, 4 words per entry (bytes 0..11, word 3 unused);
+//   window: the 8 bytes that hold the remaining positions (bytes 4..11 when
+//      n >= 8, else bytes 0..7 with positions 1..n);
+//   B: the first (up to) four window digits, C: the rest -> v_perm_b32
+//      selectors {lo, hi} of the window (out byte b = in byte sel[b]).
+// Index of a stage = its digits in mixed radix, first digit most significant;
+// the three stage indices are the mixed-radix digits (A, B, C) of the rank.
+static void build_perm_tables(int n, std::vector<uint32_t> &words, uint32_t &ra, uint32_t &rb,
+                              uint32_t &rc, int &offB, int &offC) {
+  const bool stageA = n >= 8;
+  const int base = stageA ? 4 : 0;  // first byte of the window
+  std::vector<int> pos;             // window-local positions that move
+  for (int p = stageA ? 4 : 1; p <= n; ++p) pos.push_back(p - base);
+  const int k = (int)pos.size();
+  std::vector<int> radB, radC;
+  for (int i = 0; i + 1 < k; ++i) (i < 4 ? radB : radC).push_back(k - i);
+  auto prod = [](const std::vector<int> &r) {
+    uint32_t x = 1;
+    for (int v : r) x *= (uint32_t)v;
+    return x;
+  };
+  ra = stageA ? (uint32_t)(n * (n - 1) * (n - 2)) : 1u;
+  rb = prod(radB);
+  rc = prod(radC);
+  words.clear();
+  for (uint32_t idx = 0; idx < ra; ++idx) {
+    uint8_t arr[16];
+    for (int p = 0; p < 16; ++p) arr[p] = (uint8_t)(p <= n ? p : 0);
+    if (stageA) {
+      const int d1 = (int)(idx / ((n - 1) * (n - 2))), d2 = (int)(idx / (n - 2) % (n - 1)),
+                d3 = (int)(idx % (n - 2));
+      const int d[3] = {d1, d2, d3};
+      for (int i = 1; i <= 3; ++i) std::swap(arr[i], arr[i + d[i - 1]]);
+    }
+    for (int w = 0; w < 4; ++w)
+      words.push_back((uint32_t)arr[4 * w] | (uint32_t)arr[4 * w + 1] << 8 |
+                      (uint32_t)arr[4 * w + 2] << 16 | (uint32_t)arr[4 * w + 3] << 24);
+  }
+  auto stage = [&](const std::vector<int> &rad, int first) {
+    const uint32_t R = prod(rad);
+    for (uint32_t idx = 0; idx < R; ++idx) {
+      int sel[8];
+      for (int b = 0; b < 8; ++b) sel[b] = b;
+      uint32_t rem = idx, div = R;
+      for (size_t t = 0; t < rad.size(); ++t) {
+        div /= (uint32_t)rad[t];
+        const int d = (int)(rem / div);
+        rem %= div;
+        const int i = first + (int)t;
+        std::swap(sel[pos[i]], sel[pos[i + d]]);
+      }
+      words.push_back((uint32_t)sel[0] | (uint32_t)sel[1] << 8 | (uint32_t)sel[2] << 16 |
+                      (uint32_t)sel[3] << 24);
+      words.push_back((uint32_t)sel[4] | (uint32_t)sel[5] << 8 | (uint32_t)sel[6] << 16 |
+                      (uint32_t)sel[7] << 24);
+    }
+  };
+  offB = (int)words.size();
+  stage(radB, 0);
+  offC = (int)words.size();
+  stage(radC, (int)radB.size());
+}
+
 extern "C" int qba_resource_compile(qba_ctx *ctx, int n, int kind, const int32_t *gates, int ngates,
                                     const int32_t *perm) {
   if (!ctx || n < 1 || n > QBA_MAX_PARTIES || (kind != QBA_KIND_NOTQ && kind != QBA_KIND_Q) ||
@@ -283,7 +399,14 @@ extern "C" int qba_resource_compile(qba_ctx *ctx, int n, int kind, const int32_t
     const int T = a.p.table_len + b.p.table_len;
     if (T > QBA_MAX_TABLE)
       return qba_fail(QBA_EUNSUPPORTED, "alias tables exceed the LDS budget");
-    const size_t bytes = sizeof(QbaProgramSet) + 3 * sizeof(uint64_t) * (size_t)T;
+    const bool closed = n <= QBA_CLOSED_MAX_N && notq_closed(a, n) && q_closed(b, n);
+    std::vector<uint32_t> pw;
+    uint32_t ra = 1, rb = 1, rc = 1;
+    int offB = 0, offC = 0;
+    if (closed) build_perm_tables(n, pw, ra, rb, rc, offB, offC);
+    if (pw.size() > QBA_PERM_MAX_WORDS) return qba_fail(QBA_EINVAL, "permutation tables too large");
+    const size_t perm_off = sizeof(QbaProgramSet) + 3 * sizeof(uint64_t) * (size_t)T;
+    const size_t bytes = perm_off + sizeof(uint32_t) * pw.size();
     char *img = (char *)calloc(1, bytes);
     if (!img) return qba_fail(QBA_ENOMEM, "host image");
     QbaProgramSet *ps = reinterpret_cast<QbaProgramSet *>(img);
@@ -309,6 +432,19 @@ extern "C" int qba_resource_compile(qba_ctx *ctx, int n, int kind, const int32_t
       if (Q.bits != nq || !Q.uniform || Q.col_word != 0 || Q.col_shift != 0 ||
           Q.offset != a.p.table_len || a.p.table_len != 256 * (nf - 1) + (1 << (nbits - 8 * (nf - 1))))
         ps->canonical = 0;
+    }
+    ps->closed = closed ? 1 : 0;
+    if (closed) {
+      ps->nfact = (uint32_t)factorial(n);
+      ps->t32 = (uint32_t)((1ull << 32) % ps->nfact);
+      ps->ra = ra;
+      ps->rb = rb;
+      ps->rc = rc;
+      ps->perm_off = (int32_t)perm_off;
+      ps->perm_words = (int32_t)pw.size();
+      (void)offB;
+      (void)offC;
+      memcpy(img + perm_off, pw.data(), sizeof(uint32_t) * pw.size());
     }
     uint64_t *tab = reinterpret_cast<uint64_t *>(ps + 1);
     std::copy(a.pat.begin(), a.pat.end(), tab);
@@ -358,5 +494,39 @@ extern "C" int qba_program_export(qba_ctx *ctx, int n, int kind, int32_t *n_fact
   if (pat) std::copy(hp.pat.begin(), hp.pat.end(), pat);
   if (apat) std::copy(hp.apat.begin(), hp.apat.end(), apat);
   if (thr) std::copy(hp.thr.begin(), hp.thr.end(), thr);
+  return QBA_OK;
+}
+
+extern "C" int qba_program_flags(qba_ctx *ctx, int n, int32_t *flags) {
+  if (!ctx || n < 1 || n > QBA_MAX_PARTIES || !flags)
+    return qba_fail(QBA_EINVAL, "qba_program_flags: bad arguments");
+  if (!ctx->prog_host[n]) return qba_fail(QBA_ESTATE, "qba_program_flags: not compiled");
+  const QbaProgramSet *ps = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[n]);
+  flags[0] = ps->canonical;
+  flags[1] = ps->closed;
+  flags[2] = (int32_t)ps->t32;
+  flags[3] = (int32_t)ps->ra;
+  flags[4] = (int32_t)ps->rb;
+  flags[5] = (int32_t)ps->rc;
+  return QBA_OK;
+}
+
+extern "C" int qba_perm_tables(int n, uint32_t *words, int32_t cap, int32_t *sizes) {
+  if (n < 1 || n > QBA_CLOSED_MAX_N || !sizes)
+    return qba_fail(QBA_EINVAL, "qba_perm_tables: n must be in [1, 11]");
+  std::vector<uint32_t> pw;
+  uint32_t ra, rb, rc;
+  int offB, offC;
+  build_perm_tables(n, pw, ra, rb, rc, offB, offC);
+  sizes[0] = (int32_t)ra;
+  sizes[1] = (int32_t)rb;
+  sizes[2] = (int32_t)rc;
+  sizes[3] = offB;
+  sizes[4] = offC;
+  sizes[5] = (int32_t)pw.size();
+  if (words) {
+    if (cap < (int32_t)pw.size()) return qba_fail(QBA_EINVAL, "qba_perm_tables: buffer too small");
+    std::copy(pw.begin(), pw.end(), words);
+  }
   return QBA_OK;
 }

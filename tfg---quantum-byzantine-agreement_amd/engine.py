@@ -100,12 +100,24 @@ class Engine:
         nq, _ = self.sizes(n)
         notq = resource.notQCorrelated(n, nq)
         q = resource.qCorrelated(n, nq, perm=list(range(1, n + 1)) if perm is None else perm)
+        return self.compile(n, notq, q)
+
+    def compile(self, n: int, notq: "resource.Gate", q: "resource.Gate") -> dict:
+        """Compile a (not-Q, Q) circuit pair for n parties and make it the
+        program that sample / sample_check use for n.  ``q.perm`` is the
+        permutation its X gates encode.  Returns the program info (tables and
+        the sampler flags: canonical table layout, closed form)."""
+        self._check_n(n)
+        nq, _ = self.sizes(n)
         g0 = np.ascontiguousarray(notq.triples())
         g1 = np.ascontiguousarray(q.triples())
-        p1 = np.ascontiguousarray(q.perm.astype(np.int32))
+        p1 = np.ascontiguousarray(np.asarray(q.perm, dtype=np.int32))
         call("qba_resource_compile", self.ctx, n, KIND_NOTQ, _i32p(g0), len(g0), None)
         call("qba_resource_compile", self.ctx, n, KIND_Q, _i32p(g1), len(g1), _i32p(p1))
-        info = {"n": n, "nq": nq, "notq": self.program(n, KIND_NOTQ), "q": self.program(n, KIND_Q)}
+        flags = np.zeros(6, np.int32)
+        call("qba_program_flags", self.ctx, n, _i32p(flags))
+        info = {"n": n, "nq": nq, "notq": self.program(n, KIND_NOTQ), "q": self.program(n, KIND_Q),
+                "canonical": bool(flags[0]), "closed": bool(flags[1])}
         self._prepared[n] = info
         return info
 
