@@ -342,3 +342,27 @@ def test_general_program_path(engine):
         assert bad == 0 and np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
     finally:
         engine.prepare(n, perm=list(range(1, n + 1)))
+
+
+def test_chunked_launches(monkeypatch):
+    """Launches are split into chunks of QBA_CHUNK entries (2^31; 32-bit
+    in-kernel offsets and u32 bins).  With a small chunk forced through the
+    environment, lists and counts must not change."""
+    monkeypatch.setenv("QBA_CHUNK_ENTRIES", "40000")
+    eng = sub("engine").Engine(0)
+    try:
+        n, seed, first, count = 11, 31337, 999, 123_457
+        info = eng.prepare(n)
+        lists, counts = eng.sample_check(n, seed, first, count)
+        torch.cuda.synchronize()
+        got = lists[:, :count].cpu().numpy()
+        ref = oracle_lib.sample(n, seed, first, count, info["notq"], info["q"], info["closed"])
+        assert np.array_equal(got, ref)
+        H, C, P, bad = oracle_lib.counts(ref, n)
+        gH, gC, gP = counts.numpy()
+        assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+        c2 = eng.alloc_counts(n)
+        eng.check_counts(lists, n, count, c2)
+        assert np.array_equal(c2.numpy()[0], H)
+    finally:
+        eng.close()

@@ -43,6 +43,10 @@ extern "C" int qba_init(int device, qba_ctx **out) {
   qba_ctx *ctx = new qba_ctx();
   ctx->device = device;
   ctx->num_cus = prop.multiProcessorCount;
+  if (const char *c = getenv("QBA_CHUNK_ENTRIES")) {
+    const unsigned long long v = strtoull(c, nullptr, 10) & ~3ull;
+    if (v >= 4 && v <= QBA_CHUNK) ctx->chunk = v;
+  }
   if (hipMalloc(&ctx->flag, 64) != hipSuccess || hipMalloc(&ctx->count1, 64) != hipSuccess ||
       hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess ||
       hipMalloc(&ctx->acc, (16 * 16 * 17 + 16 * 16 * 16 + 16) * 8) != hipSuccess) {

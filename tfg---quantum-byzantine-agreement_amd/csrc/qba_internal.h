@@ -15,7 +15,9 @@
 
 #define QBA_MAX_FACTORS 16
 #define QBA_MAX_TABLE 4096   // uint64 table entries per kind (LDS budget)
-#define QBA_BLOCK 256        // threads per workgroup for the list kernels
+#define QBA_BLOCK 256        // threads per workgroup (batched / helper kernels)
+#define QBA_LBLOCK 1024      // threads per workgroup of the streaming list kernels
+#define QBA_CHUNK (1ull << 31)  // entries per list-kernel launch (32-bit offsets, u32 bins)
 #define QBA_EPT 4            // entries per thread per step: one dword per list row
 
 // ---------------------------------------------------------------------------
@@ -25,14 +27,22 @@ struct QbaU4 {
   uint32_t x, y, z, w;
 };
 
-__host__ __device__ __forceinline__ QbaU4 qba_philox(uint32_t c0, uint32_t c1, uint32_t c2,
-                                                     uint32_t c3, uint32_t k0, uint32_t k1) {
+// a ^ b ^ k in one VALU op (v_bitop3_b32, truth table 0x96); k is wave-uniform
+__device__ __forceinline__ uint32_t qba_xor3(uint32_t a, uint32_t b, uint32_t k) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
+
+// Keys are wave-uniform (kernel arguments or block-uniform): they stay in SGPRs.
+__device__ __forceinline__ QbaU4 qba_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n0 = qba_xor3((uint32_t)(p1 >> 32), c1, k0);
+    const uint32_t n2 = qba_xor3((uint32_t)(p0 >> 32), c3, k1);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;
@@ -143,6 +153,7 @@ struct qba_ctx {
   int64_t *count1 = nullptr; // 1-word device counter
   int64_t *stats = nullptr;  // [2]: last counts launch: Q entries with a value >= w, spare
   void *acc = nullptr;       // int64 column sums of the slab (max bins of any n)
+  uint64_t chunk = QBA_CHUNK;  // entries per list-kernel launch (env QBA_CHUNK_ENTRIES, tests)
 };
 
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes);

@@ -25,9 +25,13 @@ struct QCfg {
   static constexpr int HB = W * G * W;    // H as returned: [u][g][x]
   static constexpr int WP = W + 1;        // LDS row stride of H: +1 word spreads banks
   static constexpr int HBL = W * G * WP;  // H as counted in LDS / the slab
-  static constexpr int CB = W * G * G;
+  static constexpr int CB = W * G * G;      // C as returned: [u][g][h]
+  static constexpr int CP = G * (G - 1) / 2; // pairs g < h, as counted
+  static constexpr int CBL = W * CP;
   static constexpr int STATS = 2;  // [0] Q entries with a value >= W (invalid), [1] spare
-  static constexpr int NBINS = HBL + CB + STATS;
+  static constexpr int NBINS = HBL + CBL + STATS;
+  // counted index of the pair g < h
+  __host__ __device__ static constexpr int pidx(int g, int h) { return g * (2 * G - g - 1) / 2 + (h - g - 1); }
   __host__ __device__ static constexpr int hidx(int u, int g, int x) { return (u * G + g) * WP + x; }
   // number of not-Q table bytes of the canonical program (ceil(n*nQ/8))
   static constexpr int NFB = (NP * NQ + 7) / 8;
@@ -302,6 +306,20 @@ __device__ __forceinline__ uint32_t qba_pk_onehot(uint32_t amt, uint32_t one) {
   return r;
 }
 
+typedef __attribute__((address_space(3))) uint32_t qba_lds_u32;  // LDS word (32-bit address)
+
+// base + byte b of x in one VALU op (v_add_u32 with an SDWA byte select)
+__device__ __forceinline__ uint32_t qba_add_byte(uint32_t base, uint32_t x, int b) {
+  uint32_t r;
+  switch (b) {
+    case 0: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(base), "v"(x)); break;
+    case 1: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(base), "v"(x)); break;
+    case 2: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(base), "v"(x)); break;
+    default: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(base), "v"(x)); break;
+  }
+  return r;
+}
+
 // ---------------------------------------------------------------------------
 // count one entry (group g = byte g % 4 of D[g / 4])
 //   Q-correlated iff L0 != L1 (tfg.py:327); u = L1 (tfg.py:182);
@@ -326,17 +344,20 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
     bad |= D[i] & vm;
   }
   if (bad) {
-    atomicAdd(&hist[C::HBL + C::CB + 0], 1u);
+    atomicAdd(&hist[C::HBL + C::CBL + 0], 1u);
     return;
   }
-  char *hb = reinterpret_cast<char *>(hist) + l1 * (uint32_t)(C::G * C::WP * 4);
+  const uint32_t hb = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist + l1 * (uint32_t)(C::G * C::WP * 4);
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) {
     const uint32_t E = D[i] << 2;  // byte b = 4 * value (< 64: no carry into the next byte)
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int g = 4 * i + b;
-      if (g < C::G) atomicAdd(reinterpret_cast<uint32_t *>(hb + ((E >> (8 * b)) & 0xffu)) + g * C::WP, 1u);
+      if (g < C::G) {
+        const uint32_t a = qba_add_byte(hb, E, b);
+        atomicAdd((uint32_t *)((qba_lds_u32 *)(uintptr_t)a + g * C::WP), 1u);
+      }
     }
   }
   uint32_t U = 0;
@@ -354,10 +375,10 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
     uint32_t l[C::G];
 #pragma unroll
     for (int g = 0; g < C::G; ++g) l[g] = (D[g / 4] >> (8 * (g % 4))) & 0xffu;
-    uint32_t *c = hist + C::HBL + l1 * (C::G * C::G);
+    uint32_t *c = hist + C::HBL + l1 * C::CP;
     for (int g = 0; g < C::G; ++g)
       for (int k = g + 1; k < C::G; ++k)
-        if (l[g] == l[k]) atomicAdd(&c[g * C::G + k], 1u);
+        if (l[g] == l[k]) atomicAdd(&c[C::pidx(g, k)], 1u);
   }
 }
 
@@ -382,7 +403,7 @@ __device__ __forceinline__ void qba_entry_d(uint64_t e, uint32_t k0, uint32_t k1
 // One thread-step: entries [c0, c0+4) of the launch (columns of `lists`).
 // MODE 0: sample -> lists;  MODE 1: sample -> lists + counts;  MODE 2: lists -> counts
 template <int NP, int MODE, int SAMP, bool TAIL>
-__device__ __forceinline__ void qba_quad(uint64_t c0, uint64_t count, uint64_t first, uint32_t k0,
+__device__ __forceinline__ void qba_quad(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                          uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                          const uint64_t *pat, const uint64_t *apat,
                                          const uint64_t *thr, const uint32_t *pl,
@@ -398,10 +419,10 @@ __device__ __forceinline__ void qba_quad(uint64_t c0, uint64_t count, uint64_t f
     if (valid == 4) {
 #pragma unroll
       for (int g = 0; g < C::G; ++g)
-        row[g] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(lists + g * ld + c0));
+        row[g] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(lists + (uint64_t)g * ld + c0));
     } else {
       for (int g = 0; g < C::G; ++g)
-        for (int j = 0; j < valid; ++j) row[g] |= (uint32_t)lists[g * ld + c0 + j] << (8 * j);
+        for (int j = 0; j < valid; ++j) row[g] |= (uint32_t)lists[(uint64_t)g * ld + c0 + j] << (8 * j);
     }
 #pragma unroll
     for (int i = 0; i < ND; ++i)
@@ -423,10 +444,10 @@ __device__ __forceinline__ void qba_quad(uint64_t c0, uint64_t count, uint64_t f
              row[4 * i + 3]);
     if (valid == 4) {
 #pragma unroll
-      for (int g = 0; g < C::G; ++g) *reinterpret_cast<uint32_t *>(lists + g * ld + c0) = row[g];
+      for (int g = 0; g < C::G; ++g) *reinterpret_cast<uint32_t *>(lists + (uint64_t)g * ld + c0) = row[g];
     } else {
       for (int g = 0; g < C::G; ++g)
-        for (int j = 0; j < valid; ++j) lists[g * ld + c0 + j] = (uint8_t)(row[g] >> (8 * j));
+        for (int j = 0; j < valid; ++j) lists[(uint64_t)g * ld + c0 + j] = (uint8_t)(row[g] >> (8 * j));
     }
   }
   if constexpr (MODE != 0) {
@@ -438,7 +459,7 @@ __device__ __forceinline__ void qba_quad(uint64_t c0, uint64_t count, uint64_t f
 }
 
 // Stage the program's tables in LDS; returns the histogram base after them.
-template <int NP, int MODE, int SAMP>
+template <int NP, int MODE, int SAMP, int BS>
 __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__ ps, uint64_t *lds,
                                                const uint64_t *&pat, const uint64_t *&apat,
                                                const uint64_t *&thr, const uint32_t *&pl) {
@@ -448,13 +469,13 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
-    for (int i = threadIdx.x; i < CF<NP>::WORDS; i += QBA_BLOCK) dst[i] = src[i];
+    for (int i = threadIdx.x; i < CF<NP>::WORDS; i += BS) dst[i] = src[i];
     hist = dst + ((CF<NP>::WORDS + 3) & ~3);
   } else if constexpr (MODE != 2) {
     const int T = ps->table_total;
     const uint64_t *tab = reinterpret_cast<const uint64_t *>(ps + 1);
     const int ntab = ps->any_nonuniform ? 3 * T : T;
-    for (int i = threadIdx.x; i < ntab; i += QBA_BLOCK) lds[i] = tab[i];
+    for (int i = threadIdx.x; i < ntab; i += BS) lds[i] = tab[i];
     apat = lds + T;
     thr = lds + 2 * T;
     hist = reinterpret_cast<uint32_t *>(lds + ntab);
@@ -463,21 +484,21 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
 }
 
 template <int NP, int MODE, int SAMP>
-__global__ void __launch_bounds__(QBA_BLOCK)
+__global__ void __launch_bounds__(QBA_LBLOCK)
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
-                uint64_t count, uint8_t *__restrict__ lists, uint64_t ld,
+                uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
                 uint32_t *__restrict__ slab) {
   using C = QCfg<NP>;
+  constexpr int BS = QBA_LBLOCK;
   extern __shared__ __align__(16) uint64_t lds[];
   const uint64_t *pat, *apat, *thr;
   const uint32_t *pl;
-  uint32_t *hist = qba_stage<NP, MODE, SAMP>(ps, lds, pat, apat, thr, pl);
+  uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
   if (MODE != 0)
-    for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
+    for (int i = threadIdx.x; i < C::NBINS; i += BS) hist[i] = 0u;
   __syncthreads();
-  const uint64_t nfull = count >> 2;
-  for (uint64_t q = (uint64_t)blockIdx.x * QBA_BLOCK + threadIdx.x; q < nfull;
-       q += (uint64_t)gridDim.x * QBA_BLOCK)
+  const uint32_t nfull = count >> 2;
+  for (uint32_t q = blockIdx.x * BS + threadIdx.x; q < nfull; q += gridDim.x * BS)
     qba_quad<NP, MODE, SAMP, false>(q << 2, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
   if ((count & 3) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
     qba_quad<NP, MODE, SAMP, true>(nfull << 2, count, first, k0, k1, ps, pat, apat, thr, pl, lists,
@@ -485,7 +506,7 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   if (MODE != 0) {
     __syncthreads();
     uint32_t *dst = slab + (size_t)blockIdx.x * C::NBINS;
-    for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) dst[i] = hist[i];
+    for (int i = threadIdx.x; i < C::NBINS; i += BS) dst[i] = hist[i];
   }
 }
 
@@ -502,26 +523,26 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   extern __shared__ __align__(16) uint64_t lds[];
   const uint64_t *pat, *apat, *thr;
   const uint32_t *pl;
-  uint32_t *hist = qba_stage<NP, 1, SAMP>(ps, lds, pat, apat, thr, pl);
+  uint32_t *hist = qba_stage<NP, 1, SAMP, QBA_BLOCK>(ps, lds, pat, apat, thr, pl);
   for (int64_t inst = blockIdx.x; inst < n_inst; inst += gridDim.x) {
     for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
     __syncthreads();
     const uint64_t key = seed_base + (uint64_t)inst;
     uint8_t *L = lists + (uint64_t)inst * inst_stride;
-    const uint64_t nfull = count >> 2;
-    for (uint64_t q = threadIdx.x; q < nfull; q += QBA_BLOCK)
-      qba_quad<NP, 1, SAMP, false>(q << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps, pat,
+    const uint32_t nfull = (uint32_t)count >> 2;
+    for (uint32_t q = threadIdx.x; q < nfull; q += QBA_BLOCK)
+      qba_quad<NP, 1, SAMP, false>(q << 2, (uint32_t)count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps, pat,
                                    apat, thr, pl, L, ld, hist);
     if ((count & 3) && threadIdx.x == 0)
-      qba_quad<NP, 1, SAMP, true>(nfull << 2, count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps,
+      qba_quad<NP, 1, SAMP, true>(nfull << 2, (uint32_t)count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps,
                                   pat, apat, thr, pl, L, ld, hist);
     __syncthreads();
     int64_t *h = H + inst * C::HB, *c = Cc + inst * C::CB, *p = P + inst * C::W;
     for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = hist[(i / C::W) * C::WP + i % C::W];
     for (int r = threadIdx.x; r < C::CB; r += QBA_BLOCK) {
       const int u = r / (C::G * C::G), g = (r / C::G) % C::G, k = r % C::G;
-      const int64_t v = g < k ? hist[C::HBL + r]
-                              : g > k ? hist[C::HBL + (u * C::G + k) * C::G + g]
+      const int64_t v = g < k ? hist[C::HBL + u * C::CP + C::pidx(g, k)]
+                              : g > k ? hist[C::HBL + u * C::CP + C::pidx(k, g)]
                                       : hist[C::hidx(u, 1, u)];
       c[r] = v;
     }
@@ -553,7 +574,7 @@ template <int NP>
 __global__ void __launch_bounds__(256)
     qba_k_finalize(const unsigned long long *__restrict__ acc, int64_t *__restrict__ H,
                    int64_t *__restrict__ Cc, int64_t *__restrict__ P, int64_t *__restrict__ stats,
-                   int accumulate) {
+                   int accumulate, int stats_accumulate) {
   using C = QCfg<NP>;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   auto put = [&](int64_t *dst, int64_t v) { *dst = accumulate ? *dst + v : v; };
@@ -565,7 +586,7 @@ __global__ void __launch_bounds__(256)
   if (r < C::CB) {
     const int u = r / (C::G * C::G), g = (r / C::G) % C::G, h = r % C::G;
     if (g < h) {
-      const int64_t v = (int64_t)acc[C::HBL + r];
+      const int64_t v = (int64_t)acc[C::HBL + u * C::CP + C::pidx(g, h)];
       put(&Cc[r], v);
       put(&Cc[(u * C::G + h) * C::G + g], v);
     } else if (g == h) {
@@ -579,7 +600,8 @@ __global__ void __launch_bounds__(256)
     return;
   }
   r -= C::W;
-  if (r < C::STATS && stats) stats[r] = (int64_t)acc[C::HBL + C::CB + r];
+  if (r < C::STATS && stats)
+    stats[r] = (stats_accumulate ? stats[r] : 0) + (int64_t)acc[C::HBL + C::CBL + r];
 }
 
 // ---------------------------------------------------------------------------
@@ -595,23 +617,26 @@ struct QbaLaunch {
   int64_t *H, *C, *P, *stats;
   int accumulate;
   hipStream_t stream;
+  int stats_accumulate;
 };
 
 static int nbins_of(int n) {
   const int g = n + 1, q = qba_nq(n), w = 1 << q;
-  return w * g * (w + 1) + w * g * g + 2;
+  return w * g * (w + 1) + w * g * (g - 1) / 2 + 2;
 }
 
-static int grid_for(qba_ctx *ctx, int mode, uint64_t count) {
+// Persistent grid: every resident workgroup slot of the chip (LDS- and
+// register-limited occupancy), fewer when the launch has less work.
+static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, QBA_LBLOCK, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
   const uint64_t nquad = (count + 3) >> 2;
-  const uint64_t per_block = (uint64_t)QBA_BLOCK * (mode == 0 ? 1 : 4);
-  uint64_t g = (nquad + per_block - 1) / per_block;
-  const uint64_t cap = (uint64_t)ctx->num_cus * (mode == 0 ? 8 : 4);
+  uint64_t g = (nquad + QBA_LBLOCK - 1) / QBA_LBLOCK;
+  const uint64_t cap = (uint64_t)ctx->num_cus * (uint64_t)per_cu;
   if (g > cap) g = cap;
   if (g < 1) g = 1;
-  // keep every per-block u32 partial far from overflow
-  const uint64_t min_g = count / (1ull << 30) + 1;
-  if (g < min_g) g = min_g;
   return (int)g;
 }
 
@@ -641,7 +666,6 @@ static int check_closed(const QbaProgramSet *hs) {
 template <int NP>
 static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
   using C = QCfg<NP>;
-  const int grid = grid_for(ctx, L.mode, L.count);
   const QbaProgramSet *hs = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP]);
   int samp = QBA_S_GENERAL;
   size_t lds = 0;
@@ -653,6 +677,23 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
   if (L.mode != 0) lds += (size_t)C::NBINS * sizeof(uint32_t);
   lds = (lds + 15) & ~(size_t)15;
   if (lds == 0) lds = 16;
+  const void *kern = nullptr;
+  if (L.mode == 2) {
+    kern = (const void *)qba_k_lists<NP, 2, QBA_S_GENERAL>;
+  } else if (samp == QBA_S_CLOSED) {
+    if constexpr (NP <= QBA_CLOSED_MAX_N)
+      kern = L.mode == 0 ? (const void *)qba_k_lists<NP, 0, QBA_S_CLOSED>
+                         : (const void *)qba_k_lists<NP, 1, QBA_S_CLOSED>;
+    else
+      return qba_fail(QBA_EUNSUPPORTED, "closed form beyond n = 11");
+  } else if (samp == QBA_S_FAST) {
+    kern = L.mode == 0 ? (const void *)qba_k_lists<NP, 0, QBA_S_FAST> : (const void *)qba_k_lists<NP, 1, QBA_S_FAST>;
+  } else {
+    kern = L.mode == 0 ? (const void *)qba_k_lists<NP, 0, QBA_S_GENERAL>
+                       : (const void *)qba_k_lists<NP, 1, QBA_S_GENERAL>;
+  }
+  if (lds > 65536) QBA_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int grid = grid_for(ctx, kern, lds, L.count);
   uint32_t *slab = nullptr;
   if (L.mode != 0) {
     int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBINS * sizeof(uint32_t));
@@ -660,27 +701,15 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
     slab = reinterpret_cast<uint32_t *>(ctx->slab);
   }
   const uint32_t k0 = (uint32_t)L.seed, k1 = (uint32_t)(L.seed >> 32);
-  auto go = [&](auto kern) -> int {
-    if (lds > 65536) QBA_HIP(hipFuncSetAttribute((const void *)kern,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(QBA_BLOCK), lds, L.stream, L.ps, k0, k1, L.first,
-                       L.count, L.lists, L.ld, slab);
-    QBA_HIP(hipGetLastError());
-    return QBA_OK;
-  };
-  int rc;
-  if (L.mode == 2) {
-    rc = go(qba_k_lists<NP, 2, QBA_S_GENERAL>);
-  } else if (samp == QBA_S_CLOSED) {
-    if constexpr (NP <= QBA_CLOSED_MAX_N)
-      rc = L.mode == 0 ? go(qba_k_lists<NP, 0, QBA_S_CLOSED>) : go(qba_k_lists<NP, 1, QBA_S_CLOSED>);
-    else
-      rc = qba_fail(QBA_EUNSUPPORTED, "closed form beyond n = 11");
-  } else if (samp == QBA_S_FAST) {
-    rc = L.mode == 0 ? go(qba_k_lists<NP, 0, QBA_S_FAST>) : go(qba_k_lists<NP, 1, QBA_S_FAST>);
-  } else {
-    rc = L.mode == 0 ? go(qba_k_lists<NP, 0, QBA_S_GENERAL>) : go(qba_k_lists<NP, 1, QBA_S_GENERAL>);
-  }
+  const QbaProgramSet *ps = L.ps;
+  uint64_t first = L.first;
+  uint32_t count = (uint32_t)L.count;
+  uint8_t *lists = L.lists;
+  uint64_t ld = L.ld;
+  void *args[] = {&ps, (void *)&k0, (void *)&k1, &first, &count, &lists, &ld, &slab};
+  QBA_HIP(hipLaunchKernel(kern, dim3(grid), dim3(QBA_LBLOCK), args, lds, L.stream));
+  QBA_HIP(hipGetLastError());
+  int rc = QBA_OK;
   if (rc || L.mode == 0) return rc;
   unsigned long long *acc = reinterpret_cast<unsigned long long *>(ctx->acc);
   QBA_HIP(hipMemsetAsync(acc, 0, sizeof(unsigned long long) * C::NBINS, L.stream));
@@ -690,7 +719,7 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
   QBA_HIP(hipGetLastError());
   const int items = C::HB + C::CB + C::W + C::STATS;
   hipLaunchKernelGGL(qba_k_finalize<NP>, dim3((items + 255) / 256), dim3(256), 0, L.stream, acc,
-                     L.H, L.C, L.P, L.stats, L.accumulate);
+                     L.H, L.C, L.P, L.stats, L.accumulate, L.stats_accumulate);
   QBA_HIP(hipGetLastError());
   return QBA_OK;
 }
@@ -780,7 +809,7 @@ extern "C" int qba_sample_check_batched(qba_ctx *ctx, int n, uint64_t seed_base,
   }
 }
 
-static int dispatch(qba_ctx *ctx, const QbaLaunch &L) {
+static int dispatch_one(qba_ctx *ctx, const QbaLaunch &L) {
   switch (L.n) {
 #define QBA_CASE(k) \
   case k:           \
@@ -792,6 +821,24 @@ static int dispatch(qba_ctx *ctx, const QbaLaunch &L) {
     default:
       return qba_fail(QBA_EUNSUPPORTED, "n_parties must be in [1, 15]");
   }
+}
+
+// Launches of at most QBA_CHUNK entries (32-bit in-kernel offsets, u32 bins);
+// chunks after the first accumulate into the caller's counts.
+static int dispatch(qba_ctx *ctx, const QbaLaunch &L0) {
+  QbaLaunch L = L0;
+  uint64_t done = 0;
+  int rc = QBA_OK;
+  do {
+    L.count = L0.count - done < ctx->chunk ? L0.count - done : ctx->chunk;
+    L.first = L0.first + done;
+    L.lists = L0.lists + done;
+    L.accumulate = done ? 1 : L0.accumulate;
+    L.stats_accumulate = done ? 1 : 0;
+    rc = dispatch_one(ctx, L);
+    done += L.count;
+  } while (!rc && done < L0.count);
+  return rc;
 }
 
 static int zero_counts(int n, int64_t *H, int64_t *C, int64_t *P, hipStream_t s) {
