@@ -184,6 +184,23 @@ __device__ __forceinline__ typename QCfg<NP>::Out qba_sample_entry_fast(
 //          permuted by B[iB] then C[iC]; group g = r ^ pi(g) (tfg.py:25-40).
 // Values are produced as bytes, group g in byte g % 4 of word g / 4.
 // ---------------------------------------------------------------------------
+// |P_u| = sum_x H[u][0][x]; H[u][1][x] = [x == u] |P_u| (group 1's own bin is
+// never counted: L1 = u by definition of the bin).
+template <int NP, typename T>
+__device__ __forceinline__ int64_t qba_psize(const T *bins, int u) {
+  using C = QCfg<NP>;
+  int64_t s = 0;
+  for (int x = 0; x < C::W; ++x) s += (int64_t)bins[C::hidx(u, 0, x)];
+  return s;
+}
+template <int NP, typename T>
+__device__ __forceinline__ int64_t qba_hval(const T *bins, int i) {  // i indexes H[u][g][x]
+  using C = QCfg<NP>;
+  const int u = i / (C::G * C::W), g = (i / C::W) % C::G, x = i % C::W;
+  if (g == 1) return x == u ? qba_psize<NP>(bins, u) : 0;
+  return (int64_t)bins[C::hidx(u, g, x)];
+}
+
 template <int NP>
 struct CF {
   using C = QCfg<NP>;
@@ -354,7 +371,7 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int g = 4 * i + b;
-      if (g < C::G) {
+      if (g < C::G && g != 1) {  // H[u][1][x] = [x == u] |P_u|, derived when reduced
         const uint32_t a = qba_add_byte(hb, E, b);
         atomicAdd((uint32_t *)((qba_lds_u32 *)(uintptr_t)a + g * C::WP), 1u);
       }
@@ -538,15 +555,15 @@ __global__ void __launch_bounds__(QBA_BLOCK)
                                   pat, apat, thr, pl, L, ld, hist);
     __syncthreads();
     int64_t *h = H + inst * C::HB, *c = Cc + inst * C::CB, *p = P + inst * C::W;
-    for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = hist[(i / C::W) * C::WP + i % C::W];
+    for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = qba_hval<NP>(hist, i);
     for (int r = threadIdx.x; r < C::CB; r += QBA_BLOCK) {
       const int u = r / (C::G * C::G), g = (r / C::G) % C::G, k = r % C::G;
       const int64_t v = g < k ? hist[C::HBL + u * C::CP + C::pidx(g, k)]
                               : g > k ? hist[C::HBL + u * C::CP + C::pidx(k, g)]
-                                      : hist[C::hidx(u, 1, u)];
+                                      : qba_psize<NP>(hist, u);
       c[r] = v;
     }
-    for (int u = threadIdx.x; u < C::W; u += QBA_BLOCK) p[u] = hist[C::hidx(u, 1, u)];
+    for (int u = threadIdx.x; u < C::W; u += QBA_BLOCK) p[u] = qba_psize<NP>(hist, u);
     __syncthreads();
   }
 }
@@ -579,7 +596,7 @@ __global__ void __launch_bounds__(256)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   auto put = [&](int64_t *dst, int64_t v) { *dst = accumulate ? *dst + v : v; };
   if (i < C::HB) {
-    put(&H[i], (int64_t)acc[(i / C::W) * C::WP + i % C::W]);
+    put(&H[i], qba_hval<NP>(acc, i));
     return;
   }
   int r = i - C::HB;
@@ -590,13 +607,13 @@ __global__ void __launch_bounds__(256)
       put(&Cc[r], v);
       put(&Cc[(u * C::G + h) * C::G + g], v);
     } else if (g == h) {
-      put(&Cc[r], (int64_t)acc[C::hidx(u, 1, u)]);
+      put(&Cc[r], qba_psize<NP>(acc, u));
     }
     return;
   }
   r -= C::CB;
   if (r < C::W) {
-    put(&P[r], (int64_t)acc[C::hidx(r, 1, r)]);
+    put(&P[r], qba_psize<NP>(acc, r));
     return;
   }
   r -= C::W;
