@@ -156,47 +156,58 @@ static uint64_t sample_outcome(int n, uint64_t seed, uint64_t e, const prog_t *n
 
 /* Closed-form schedule (csrc/qba_lists.hip, "Closed-form sampler"), used by
  * the engine for n <= 11 when both programs are proven to be tfg.py's
- * circuits' distributions.  Restated here from its definition: the rank
+ * circuits' distributions.  Restated here from its definition: entry e uses
+ * the 64-bit half e & 1 of the Philox block of its pair e >> 1; the rank
  * R = floor(F * n! / 2^32) is decoded directly into forward Fisher-Yates
  * digits (the engine instead splits it into three table indices). */
+static int lemire_ok(uint32_t F, uint32_t nfact, uint32_t t) { return (uint32_t)(F * nfact) >= t; }
+
 static void closed_entry(int n, uint64_t seed, uint64_t e, uint8_t vals[16]) {
   const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-  const uint32_t ctr[4] = {(uint32_t)e, (uint32_t)(e >> 32), 0u, 0u};
+  const uint64_t p = e >> 1;
+  const uint32_t h = (uint32_t)(e & 1);
+  const uint32_t ctr[4] = {(uint32_t)p, (uint32_t)(p >> 32), 0u, 0u};
   uint32_t x[4];
   philox4x32_10(ctr, key, x);
+  const uint32_t w0 = x[2 * h], w1 = x[2 * h + 1];
   const int nq = n_qubits(n);
   const uint32_t W = 1u << nq;
-  if (!(x[0] & 1u)) { /* not-Q: L0 = L1, L1..Ln independent uniform */
-    uint32_t v[16];
-    for (int b = 0; b < 4; ++b) {
-      v[b] = (x[1] >> (8 * b)) & (W - 1);
-      v[4 + b] = (x[1] >> (8 * b + 4)) & (W - 1);
-      v[8 + b] = (x[2] >> (8 * b)) & (W - 1);
-      v[12 + b] = (x[2] >> (8 * b + 4)) & (W - 1);
-    }
+  if (!(w0 & 1u)) { /* not-Q: L0 = L1, L1..Ln independent uniform */
+    static const int w1_shift[8] = {0, 8, 16, 24, 4, 12, 20, 28};
+    static const int w0_shift[6] = {8, 16, 24, 12, 20, 28};
+    uint32_t v[14];
+    for (int i = 0; i < 8; ++i) v[i] = (w1 >> w1_shift[i]) & (W - 1);
+    for (int i = 0; i < 6; ++i) v[8 + i] = (w0 >> w0_shift[i]) & (W - 1);
     vals[0] = (uint8_t)v[0];
     for (int g = 1; g <= n; ++g) vals[g] = (uint8_t)v[g - 1];
     return;
   }
   uint32_t nfact = 1;
   for (int i = 2; i <= n; ++i) nfact *= (uint32_t)i;
-  const uint32_t t = (uint32_t)((1ull << 32) % nfact);
-  uint32_t cand[4] = {x[2], x[3], 0, 0};
-  int nc = 2, ci = 0;
-  uint32_t a = 0, F = 0;
-  for (;;) {
-    if (ci == nc) {
-      const uint32_t c2[4] = {(uint32_t)e, (uint32_t)(e >> 32), 0x80000000u + ++a, 0u};
-      philox4x32_10(c2, key, cand);
-      nc = 4;
-      ci = 0;
+  const uint32_t t32 = (uint32_t)((1ull << 32) % nfact);
+  const uint32_t t27 = (uint32_t)(((1ull << 27) % nfact) << 5);
+  uint32_t F;
+  if (lemire_ok(w1, nfact, t32)) {
+    F = w1;
+  } else if (lemire_ok(w0 & ~31u, nfact, t27)) {
+    F = w0 & ~31u;
+  } else {
+    int found = 0;
+    F = 0;
+    for (uint32_t a = 1; !found; ++a) {
+      const uint32_t c2[4] = {(uint32_t)p, (uint32_t)(p >> 32), 0x80000000u + a, h};
+      uint32_t y[4];
+      philox4x32_10(c2, key, y);
+      for (int i = 0; i < 4 && !found; ++i)
+        if (lemire_ok(y[i], nfact, t32)) {
+          F = y[i];
+          found = 1;
+        }
     }
-    F = cand[ci++];
-    if ((uint32_t)(F * nfact) >= t) break;
   }
   uint32_t R = (uint32_t)(((uint64_t)F * nfact) >> 32);
   int perm[16];
-  for (int p = 0; p < 16; ++p) perm[p] = p;
+  for (int q = 0; q < 16; ++q) perm[q] = q;
   uint32_t div = nfact;
   for (int i = 1; i < n; ++i) { /* digit of position i has radix n - i + 1 */
     div /= (uint32_t)(n - i + 1);
@@ -206,7 +217,7 @@ static void closed_entry(int n, uint64_t seed, uint64_t e, uint8_t vals[16]) {
     perm[i] = perm[j];
     perm[j] = tmp;
   }
-  const uint32_t r = (x[0] >> 1) & (W - 1);
+  const uint32_t r = (w0 >> 1) & (W - 1);
   for (int g = 0; g <= n; ++g) vals[g] = (uint8_t)(r ^ (uint32_t)perm[g]);
 }
 

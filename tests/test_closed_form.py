@@ -74,27 +74,60 @@ def closed_entry_py(n, seed, e):
     """Python restatement of the closed-form schedule for one entry."""
     nq = oracle_lib.n_qubits(n)
     W = 1 << nq
-    x = [int(v) for v in oracle_lib.philox(np.array([e & 0xFFFFFFFF, e >> 32, 0, 0], np.uint32), seed)[0]]
-    if not x[0] & 1:
-        vals = [(x[1] >> (8 * b)) & (W - 1) for b in range(4)] + \
-               [(x[1] >> (8 * b + 4)) & (W - 1) for b in range(4)] + \
-               [(x[2] >> (8 * b)) & (W - 1) for b in range(4)] + \
-               [(x[2] >> (8 * b + 4)) & (W - 1) for b in range(4)]
+    p, h = e >> 1, e & 1
+    x = [int(v) for v in oracle_lib.philox(np.array([p & 0xFFFFFFFF, p >> 32, 0, 0], np.uint32), seed)[0]]
+    w0, w1 = x[2 * h], x[2 * h + 1]
+    if not w0 & 1:
+        vals = [(w1 >> s) & (W - 1) for s in (0, 8, 16, 24, 4, 12, 20, 28)] + \
+               [(w0 >> s) & (W - 1) for s in (8, 16, 24, 12, 20, 28)]
         return [vals[0]] + vals[: n]
     nf = math.factorial(n)
-    t = (1 << 32) % nf
-    cands, a = [x[2], x[3]], 0
-    while True:
-        if not cands:
+    t32, t27 = (1 << 32) % nf, ((1 << 27) % nf) << 5
+    ok = lambda F, t: (F * nf) & 0xFFFFFFFF >= t  # noqa: E731
+    if ok(w1, t32):
+        F = w1
+    elif ok(w0 & ~31 & 0xFFFFFFFF, t27):
+        F = w0 & ~31 & 0xFFFFFFFF
+    else:
+        a, F = 0, None
+        while F is None:
             a += 1
-            cands = [int(v) for v in oracle_lib.philox(
-                np.array([e & 0xFFFFFFFF, e >> 32, 0x80000000 + a, 0], np.uint32), seed)[0]]
-        F = cands.pop(0)
-        if (F * nf) & 0xFFFFFFFF >= t:
-            break
+            ys = [int(v) for v in oracle_lib.philox(
+                np.array([p & 0xFFFFFFFF, p >> 32, 0x80000000 + a, h], np.uint32), seed)[0]]
+            F = next((y for y in ys if ok(y, t32)), None)
     perm = fy_decode(n, (F * nf) >> 32)
-    r = (x[0] >> 1) & (W - 1)
-    return [r ^ p for p in perm]
+    r = (w0 >> 1) & (W - 1)
+    return [r ^ q for q in perm]
+
+
+def test_closed_rank_fallbacks():
+    """The 27-bit second candidate and the retry blocks are reached: find
+    entries of each kind at n = 11 and check the oracle against the Python
+    restatement there."""
+    n, seed = 11, 5
+    nf = math.factorial(n)
+    t32, t27 = (1 << 32) % nf, ((1 << 27) % nf) << 5
+    ctr = np.zeros((1 << 16, 4), np.uint32)
+    ctr[:, 0] = np.arange(1 << 16)
+    x = oracle_lib.philox(ctr, seed).astype(np.uint64)
+    kinds = {}
+    for p in range(1 << 16):
+        for h in (0, 1):
+            w0, w1 = int(x[p, 2 * h]), int(x[p, 2 * h + 1])
+            if not w0 & 1:
+                continue
+            if (w1 * nf) & 0xFFFFFFFF >= t32:
+                kinds.setdefault("w1", 2 * p + h)
+            elif ((w0 & ~31 & 0xFFFFFFFF) * nf) & 0xFFFFFFFF >= t27:
+                kinds.setdefault("w0", 2 * p + h)
+            else:
+                kinds.setdefault("retry", 2 * p + h)
+    assert {"w1", "w0"} <= set(kinds)
+    info = {"nfac": 0, "desc": np.zeros((0, 6), np.int32), "pat": np.zeros(1, np.uint64),
+            "apat": np.zeros(1, np.uint64), "thr": np.zeros(1, np.uint64)}
+    for e in kinds.values():
+        got = oracle_lib.sample(n, seed, e, 1, info, info, closed=True)
+        assert list(got[:, 0]) == closed_entry_py(n, seed, e)
 
 
 @pytest.mark.parametrize("n", [1, 3, 7, 8, 11])

@@ -27,16 +27,18 @@ struct QbaU4 {
   uint32_t x, y, z, w;
 };
 
-// a ^ b ^ k in one VALU op (v_bitop3_b32, truth table 0x96); k is wave-uniform
+// a ^ b ^ k in one VALU op (v_bitop3_b32, truth table 0x96)
 __device__ __forceinline__ uint32_t qba_xor3(uint32_t a, uint32_t b, uint32_t k) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
-  return r;
+  return __builtin_amdgcn_bitop3_b32(a, b, k, 0x96);
 }
 
 // Keys are wave-uniform (kernel arguments or block-uniform): they stay in SGPRs.
 __device__ __forceinline__ QbaU4 qba_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                             uint32_t k0, uint32_t k1) {
+#ifdef QBA_EXP_CHEAPRNG  // experiment builds only (tools/exp): cost of the generator
+  const uint32_t h = (c0 ^ k0) * 0x9E3779B9u + c1 + c2 * 0x85EBCA6Bu;
+  return QbaU4{h, h * 0xC2B2AE35u, h ^ (h >> 15) ^ k1, (h * 0x27D4EB2Fu) ^ c3};
+#endif
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;

@@ -16,6 +16,11 @@
 
 #include "qba_internal.h"
 
+// Experiment builds only (tools/exp): restrict instantiation to one n.
+#ifndef QBA_ONLY_N
+#define QBA_ONLY_N 0
+#endif
+
 template <int NP>
 struct QCfg {
   static constexpr int G = NP + 1;  // measured groups (n parties + the commander's extra)
@@ -170,18 +175,23 @@ __device__ __forceinline__ typename QCfg<NP>::Out qba_sample_entry_fast(
 }
 
 // ---------------------------------------------------------------------------
-// Closed-form sampler (QbaProgramSet::closed; n <= 11).  Per entry e:
-//   x = philox(ctr = {e_lo, e_hi, 0, 0}, key = seed);  isQ = x0 & 1
-//   not-Q: values v_0..v_15 = the nQ low bits of the bytes of x1, x1 >> 4,
-//          x2, x2 >> 4 (in that order); group g >= 1 takes v_{g-1}, group 0
-//          takes v_0 (= group 1, tfg.py:15-22).
-//   Q:     r = (x0 >> 1) & (W-1); the rank F is the first of x2, x3 whose
-//          F * n! mod 2^32 >= 2^32 mod n! (Lemire: exactly uniform); if both
-//          fail, the words of philox(ctr = {e_lo, e_hi, 0x80000000 + a, 0})
-//          for a = 1, 2, ... in order.  (iA, iB, iC) = the mixed-radix digits
-//          of floor(F * n! / 2^32) in radices (RA, RB, RC) [F * RA = iA:F1,
-//          F1 * RB = iB:F2, F2 * RC = iC:F3], pi = stage A[iA] with its window
-//          permuted by B[iB] then C[iC]; group g = r ^ pi(g) (tfg.py:25-40).
+// Closed-form sampler (QbaProgramSet::closed; n <= 11).  Entries come in
+// pairs: entry e uses half h = e & 1 of block
+//   x = philox(ctr = {p_lo, p_hi, 0, 0}, key = seed),  p = e >> 1,
+// i.e. the 64 bits w0 = x[2h], w1 = x[2h+1].  isQ = w0 & 1.
+//   not-Q: values v_0..v_13 = the nQ low bits of the nibbles at bits
+//          {0,8,16,24, 4,12,20,28} of w1 then {8,16,24, 12,20,28} of w0;
+//          group g >= 1 takes v_{g-1}, group 0 takes v_0 (= group 1,
+//          tfg.py:15-22).
+//   Q:     r = (w0 >> 1) & (W-1).  The rank word F is w1 if
+//          F * n! mod 2^32 >= 2^32 mod n!, else w0 & ~31 (bits 5..31, a
+//          27-bit fraction) if F * n! mod 2^32 >= (2^27 mod n!) << 5 (Lemire on
+//          27 bits), else the words of philox(ctr = {p_lo, p_hi, 0x80000000 + a,
+//          h}) for a = 1, 2, ... in order (32-bit test): exactly uniform.
+//          (iA, iB, iC) = the mixed-radix digits of floor(F * n! / 2^32) in
+//          radices (RA, RB, RC) [F * RA = iA:F1, F1 * RB = iB:F2, F2 * RC =
+//          iC:F3], pi = stage A[iA] with its window permuted by B[iB] then
+//          C[iC]; group g = r ^ pi(g) (tfg.py:25-40).
 // Values are produced as bytes, group g in byte g % 4 of word g / 4.
 // ---------------------------------------------------------------------------
 // |P_u| = sum_x H[u][0][x]; H[u][1][x] = [x == u] |P_u| (group 1's own bin is
@@ -218,6 +228,7 @@ struct CF {
   static constexpr uint32_t RC = K >= 6 ? fact(K - 4, 2) : 1u;
   static constexpr uint32_t NFACT = fact(NP, 2);
   static constexpr uint32_t T32 = (uint32_t)((1ull << 32) % NFACT);
+  static constexpr uint32_t T27 = (uint32_t)(((1ull << 27) % NFACT) << 5);  // 27-bit test, scaled
   static constexpr int OFFB = 4 * (int)RA;            // in words
   static constexpr int OFFC = OFFB + 2 * (int)RB;
   static constexpr int WORDS = OFFC + 2 * (int)RC;
@@ -228,69 +239,90 @@ __device__ __forceinline__ uint32_t qba_perm_b(uint32_t hi, uint32_t lo, uint32_
   return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
-// first acceptable rank word among a, b (Lemire test); ok = 0 if neither
+// Lemire acceptance of a 32-bit rank word against threshold T (scaled)
 template <int NP>
-__device__ __forceinline__ uint32_t qba_pick2(uint32_t a, uint32_t b, bool &ok) {
-  using F = CF<NP>;
-  const bool oa = a * F::NFACT >= F::T32, ob = b * F::NFACT >= F::T32;
-  ok = oa || ob;
-  return oa ? a : b;
+__device__ __forceinline__ bool qba_accept(uint32_t F, uint32_t T) {
+  return F * CF<NP>::NFACT >= T;
 }
 
+// One entry from its 64 random bits (w0, w1); (p, h) identify it for the
+// (rare) rank retry.
 template <int NP>
-__device__ __forceinline__ void qba_closed_entry(uint64_t e, uint32_t k0, uint32_t k1,
-                                                 const uint32_t *__restrict__ pl,
-                                                 uint32_t (&D)[CF<NP>::ND]) {
+__device__ __forceinline__ void qba_closed_half(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
+                                                uint32_t k0, uint32_t k1,
+                                                const uint32_t *__restrict__ pl,
+                                                uint32_t (&D)[CF<NP>::ND]) {
   using F = CF<NP>;
-  const uint32_t elo = (uint32_t)e, ehi = (uint32_t)(e >> 32);
-  const QbaU4 x = qba_philox(elo, ehi, 0u, 0u, k0, k1);
   // not-Q words
   uint32_t nq[4];
   {
-    const uint32_t a = x.y & F::M4, b = (x.y >> 4) & F::M4, c = x.z & F::M4, d = (x.z >> 4) & F::M4;
+    const uint32_t a = w1 & F::M4, b = (w1 >> 4) & F::M4, c = (w0 >> 8) & F::M4, d = (w0 >> 12) & F::M4;
     nq[0] = qba_perm_b(a, a, 0x02010000u);
     nq[1] = qba_perm_b(b, a, 0x06050403u);
     nq[2] = qba_perm_b(c, b, 0x06050403u);
     nq[3] = qba_perm_b(d, c, 0x06050403u);
   }
   // Q words
-  bool ok;
-  uint32_t rank = qba_pick2<NP>(x.z, x.w, ok);
-  if (__builtin_expect(!ok, 0)) {  // probability (T32 / 2^32)^2 per Q entry
+  const bool o1 = qba_accept<NP>(w1, F::T32);
+  uint32_t rank = o1 ? w1 : (w0 & ~31u);
+  if (__builtin_expect(!o1 && !qba_accept<NP>(rank, F::T27), 0)) {  // ~(T32 T27) / 2^59 per Q entry
+    bool ok = false;
     for (uint32_t a = 1; !ok; ++a) {
-      const QbaU4 y = qba_philox(elo, ehi, 0x80000000u + a, 0u, k0, k1);
-      bool o1, o2;
-      const uint32_t r1 = qba_pick2<NP>(y.x, y.y, o1), r2 = qba_pick2<NP>(y.z, y.w, o2);
-      ok = o1 || o2;
-      rank = o1 ? r1 : r2;
+      const QbaU4 y = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0x80000000u + a, h, k0, k1);
+      const uint32_t c[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (!ok && qba_accept<NP>(c[i], F::T32)) {
+          ok = true;
+          rank = c[i];
+        }
     }
   }
   uint32_t iA = 0, rem = rank;
   if constexpr (F::RA > 1) {
-    const uint64_t p = (uint64_t)rem * F::RA;
-    iA = (uint32_t)(p >> 32);
-    rem = (uint32_t)p;
+    const uint64_t pa = (uint64_t)rem * F::RA;
+    iA = (uint32_t)(pa >> 32);
+    rem = (uint32_t)pa;
   }
   const uint64_t pb = (uint64_t)rem * F::RB;
   const uint32_t iB = (uint32_t)(pb >> 32);
+#ifdef QBA_EXP_NOTABLE
+  const uint4 A = make_uint4(iA, iA * 3u, iA * 5u, 0u);
+  const uint2 sB = make_uint2(iB, iB * 7u);
+#else
   const uint4 A = *reinterpret_cast<const uint4 *>(pl + 4 * iA);
   const uint2 sB = *reinterpret_cast<const uint2 *>(pl + F::OFFB + 2 * iB);
+#endif
   uint32_t q[4] = {A.x, A.y, A.z, A.w};
-  uint32_t w0 = q[F::WIN], w1 = q[F::WIN + 1];
-  uint32_t y0 = qba_perm_b(w1, w0, sB.x), y1 = qba_perm_b(w1, w0, sB.y);
+  uint32_t y0 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.x), y1 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.y);
   if constexpr (F::RC > 1) {
     const uint32_t iC = (uint32_t)(((uint64_t)(uint32_t)pb * F::RC) >> 32);
+#ifdef QBA_EXP_NOTABLE
+    const uint2 sC = make_uint2(iC, iC * 9u);
+#else
     const uint2 sC = *reinterpret_cast<const uint2 *>(pl + F::OFFC + 2 * iC);
+#endif
     const uint32_t z0 = qba_perm_b(y1, y0, sC.x), z1 = qba_perm_b(y1, y0, sC.y);
     y0 = z0;
     y1 = z1;
   }
   q[F::WIN] = y0;
   q[F::WIN + 1] = y1;
-  const uint32_t R = ((x.x >> 1) & (uint32_t)(QCfg<NP>::W - 1)) * 0x01010101u;
-  const bool isq = x.x & 1u;
+  const uint32_t R = ((w0 >> 1) & (uint32_t)(QCfg<NP>::W - 1)) * 0x01010101u;
+  const bool isq = w0 & 1u;
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) D[i] = isq ? (q[i] ^ R) : nq[i];
+}
+
+// Entry e on its own (odd pair alignment, tails): the half of its pair's block.
+template <int NP>
+__device__ __forceinline__ void qba_closed_entry(uint64_t e, uint32_t k0, uint32_t k1,
+                                                 const uint32_t *__restrict__ pl,
+                                                 uint32_t (&D)[CF<NP>::ND]) {
+  const uint64_t p = e >> 1;
+  const uint32_t h = (uint32_t)e & 1u;
+  const QbaU4 x = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0u, 0u, k0, k1);
+  qba_closed_half<NP>(h ? x.z : x.x, h ? x.w : x.y, p, h, k0, k1, pl, D);
 }
 
 // Outcome word of the table samplers -> byte layout.
@@ -351,6 +383,9 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
   using F = CF<NP>;
   const uint32_t l0 = D[0] & 0xffu, l1 = (D[0] >> 8) & 0xffu;
   if (l0 == l1) return;
+#ifdef QBA_EXP_NOCOUNT
+  if (l0 != 0xfffu) return;
+#endif
   uint32_t bad = 0;
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) {
@@ -377,6 +412,9 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
       }
     }
   }
+#ifdef QBA_EXP_NOSEEN
+  return;
+#endif
   uint32_t U = 0;
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) {
@@ -446,20 +484,41 @@ __device__ __forceinline__ void qba_quad(uint32_t c0, uint32_t count, uint64_t f
       qba_t4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3], D[0][i], D[1][i], D[2][i],
              D[3][i]);
   } else {
+    bool done = false;
+    if constexpr (SAMP == QBA_S_CLOSED && !TAIL) {
+      if (!(first & 1)) {  // wave-uniform: the quad is two whole pairs
+        const uint64_t p0 = (first + c0) >> 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j < valid) {
-        qba_entry_d<NP, SAMP>(first + c0 + j, k0, k1, ps, pat, apat, thr, pl, D[j]);
-      } else {
+        for (int jp = 0; jp < 2; ++jp) {
+          const uint64_t p = p0 + jp;
+          const QbaU4 x = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0u, 0u, k0, k1);
+          qba_closed_half<NP>(x.x, x.y, p, 0u, k0, k1, pl, D[2 * jp]);
+          qba_closed_half<NP>(x.z, x.w, p, 1u, k0, k1, pl, D[2 * jp + 1]);
+        }
+        done = true;
+      }
+    }
+    if (!done) {
 #pragma unroll
-        for (int i = 0; i < ND; ++i) D[j][i] = 0;
+      for (int j = 0; j < 4; ++j) {
+        if (j < valid) {
+          qba_entry_d<NP, SAMP>(first + c0 + j, k0, k1, ps, pat, apat, thr, pl, D[j]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < ND; ++i) D[j][i] = 0;
+        }
       }
     }
 #pragma unroll
     for (int i = 0; i < ND; ++i)
       qba_t4(D[0][i], D[1][i], D[2][i], D[3][i], row[4 * i], row[4 * i + 1], row[4 * i + 2],
              row[4 * i + 3]);
-    if (valid == 4) {
+#ifdef QBA_EXP_NOSTORE
+    if (row[0] == 0x12345678u && row[1] == 0x9abcdef0u)
+#else
+    if (valid == 4)
+#endif
+    {
 #pragma unroll
       for (int g = 0; g < C::G; ++g) *reinterpret_cast<uint32_t *>(lists + (uint64_t)g * ld + c0) = row[g];
     } else {
@@ -816,6 +875,7 @@ extern "C" int qba_sample_check_batched(qba_ctx *ctx, int n, uint64_t seed_base,
   switch (n) {
 #define QBA_CASE(k) \
   case k:           \
+    if (QBA_ONLY_N && k != QBA_ONLY_N) return qba_fail(QBA_EUNSUPPORTED, "experiment build"); \
     return launch_batched_np<k>(ctx, B);
     QBA_CASE(1) QBA_CASE(2) QBA_CASE(3) QBA_CASE(4) QBA_CASE(5) QBA_CASE(6) QBA_CASE(7)
     QBA_CASE(8) QBA_CASE(9) QBA_CASE(10) QBA_CASE(11) QBA_CASE(12) QBA_CASE(13) QBA_CASE(14)
@@ -830,6 +890,7 @@ static int dispatch_one(qba_ctx *ctx, const QbaLaunch &L) {
   switch (L.n) {
 #define QBA_CASE(k) \
   case k:           \
+    if (QBA_ONLY_N && k != QBA_ONLY_N) return qba_fail(QBA_EUNSUPPORTED, "experiment build"); \
     return launch_np<k>(ctx, L);
     QBA_CASE(1) QBA_CASE(2) QBA_CASE(3) QBA_CASE(4) QBA_CASE(5) QBA_CASE(6) QBA_CASE(7)
     QBA_CASE(8) QBA_CASE(9) QBA_CASE(10) QBA_CASE(11) QBA_CASE(12) QBA_CASE(13) QBA_CASE(14)
