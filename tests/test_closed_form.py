@@ -52,8 +52,9 @@ def compose(n, sizes, words, R):
     w0, w1 = q[win], q[win + 1]
     sb = words[offb + 2 * iB: offb + 2 * iB + 2]
     y0, y1 = vperm(w1, w0, int(sb[0])), vperm(w1, w0, int(sb[1]))
-    sc = words[offc + 2 * iC: offc + 2 * iC + 2]
-    q[win], q[win + 1] = vperm(y1, y0, int(sc[0])), vperm(y1, y0, int(sc[1]))
+    if rc > 1:  # C stores its hi selector only (its swaps stay in window bytes 4..7)
+        y1 = vperm(y1, y0, int(words[offc + iC]))
+    q[win], q[win + 1] = y0, y1
     return [(q[g // 4] >> (8 * (g % 4))) & 0xFF for g in range(n + 1)]
 
 
@@ -62,6 +63,7 @@ def test_stage_tables_compose_to_fisher_yates(n):
     sizes, words = tables(n)
     ra, rb, rc = (int(x) for x in sizes[:3])
     assert ra * rb * rc == math.factorial(n)
+    assert int(sizes[5]) == 4 * ra + 2 * rb + rc  # A [ra][4], B [rb][2], C [rc] (hi selector)
     assert ra == (n * (n - 1) * (n - 2) if n >= 8 else 1)
     nf = math.factorial(n)
     ranks = range(nf) if nf <= 40320 else \

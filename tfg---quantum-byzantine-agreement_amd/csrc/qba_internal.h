@@ -112,11 +112,11 @@ struct QbaProgramSet {
   uint32_t nfact;           // n!
   uint32_t ra, rb, rc;      // stage sizes, ra * rb * rc = n!
   int32_t perm_off;         // byte offset of the stage tables from the image start
-  int32_t perm_words;       // u32 words of stage tables: A [ra][4], B [rb][2], C [rc][2]
+  int32_t perm_words;       // u32 words of stage tables: A [ra][4], B [rb][2], C [rc] (hi only)
 };
 
-// Closed-form stage tables (host-built, staged to LDS): 4 + 2 + 2 words per
-// entry of A, B, C.  Largest: n = 11 -> 990*4 + 1680*2 + 24*2 = 7368 words.
+// Closed-form stage tables (host-built, staged to LDS): 4 + 2 + 1 words per
+// entry of A, B, C.  Largest: n = 11 -> 990*4 + 1680*2 + 24 = 7344 words.
 #define QBA_PERM_MAX_WORDS 7400
 #define QBA_CLOSED_MAX_N 11
 

@@ -231,7 +231,7 @@ struct CF {
   static constexpr uint32_t T27 = (uint32_t)(((1ull << 27) % NFACT) << 5);  // 27-bit test, scaled
   static constexpr int OFFB = 4 * (int)RA;            // in words
   static constexpr int OFFC = OFFB + 2 * (int)RB;
-  static constexpr int WORDS = OFFC + 2 * (int)RC;
+  static constexpr int WORDS = OFFC + (int)RC;  // C keeps only its hi selector
   static constexpr uint32_t M4 = (uint32_t)(C::W - 1) * 0x01010101u;
 };
 
@@ -245,39 +245,65 @@ __device__ __forceinline__ bool qba_accept(uint32_t F, uint32_t T) {
   return F * CF<NP>::NFACT >= T;
 }
 
-// One entry from its 64 random bits (w0, w1); (p, h) identify it for the
-// (rare) rank retry.
-template <int NP>
-__device__ __forceinline__ void qba_closed_half(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
-                                                uint32_t k0, uint32_t k1,
-                                                const uint32_t *__restrict__ pl,
-                                                uint32_t (&D)[CF<NP>::ND]) {
-  using F = CF<NP>;
-  // not-Q words
+// One entry from its 64 random bits (w0, w1), in two phases so that a quad's
+// table reads are issued together: qba_closed_rank (not-Q words, Lemire rank;
+// (p, h) identify the entry for the rare retry) then qba_closed_finish.
+struct QbaClosed {
   uint32_t nq[4];
-  {
-    const uint32_t a = w1 & F::M4, b = (w1 >> 4) & F::M4, c = (w0 >> 8) & F::M4, d = (w0 >> 12) & F::M4;
-    nq[0] = qba_perm_b(a, a, 0x02010000u);
-    nq[1] = qba_perm_b(b, a, 0x06050403u);
-    nq[2] = qba_perm_b(c, b, 0x06050403u);
-    nq[3] = qba_perm_b(d, c, 0x06050403u);
-  }
-  // Q words
+  uint32_t rank, w0;
+};
+
+template <int NP>
+__device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
+                                                uint32_t k0, uint32_t k1, QbaClosed &c) {
+  using F = CF<NP>;
+  const uint32_t a = w1 & F::M4, b = (w1 >> 4) & F::M4, cc = (w0 >> 8) & F::M4, d = (w0 >> 12) & F::M4;
+  c.nq[0] = qba_perm_b(a, a, 0x02010000u);
+  c.nq[1] = qba_perm_b(b, a, 0x06050403u);
+  c.nq[2] = qba_perm_b(cc, b, 0x06050403u);
+  c.nq[3] = qba_perm_b(d, cc, 0x06050403u);
+  c.w0 = w0;
   const bool o1 = qba_accept<NP>(w1, F::T32);
   uint32_t rank = o1 ? w1 : (w0 & ~31u);
-  if (__builtin_expect(!o1 && !qba_accept<NP>(rank, F::T27), 0)) {  // ~(T32 T27) / 2^59 per Q entry
+  if (__builtin_expect(!o1 && !qba_accept<NP>(rank, F::T27), 0)) {  // ~(T32 T27) / 2^59 per entry
     bool ok = false;
-    for (uint32_t a = 1; !ok; ++a) {
-      const QbaU4 y = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0x80000000u + a, h, k0, k1);
-      const uint32_t c[4] = {y.x, y.y, y.z, y.w};
+    for (uint32_t t = 1; !ok; ++t) {
+      const QbaU4 y = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0x80000000u + t, h, k0, k1);
+      const uint32_t cand[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (!ok && qba_accept<NP>(c[i], F::T32)) {
+        if (!ok && qba_accept<NP>(cand[i], F::T32)) {
           ok = true;
-          rank = c[i];
+          rank = cand[i];
         }
     }
   }
+  c.rank = rank;
+}
+
+template <int NP>
+__device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint4 &A, const uint2 &sB,
+                                                  uint32_t sC, uint32_t (&D)[CF<NP>::ND]) {
+  using F = CF<NP>;
+  // A.w is zero in the table; folding it in keeps the read one ds_read_b128
+  // (4 LDS cycles) instead of a ds_read_b96 (8).
+  uint32_t q[4] = {A.x | A.w, A.y, A.z, A.w};
+  const uint32_t y0 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.x);
+  uint32_t y1 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.y);
+  if constexpr (F::RC > 1) y1 = qba_perm_b(y1, y0, sC);  // stage C moves window bytes 4..7 only
+  q[F::WIN] = y0;
+  q[F::WIN + 1] = y1;
+  const uint32_t R = ((c.w0 >> 1) & (uint32_t)(QCfg<NP>::W - 1)) * 0x01010101u;
+  const uint32_t qm = 0u - (c.w0 & 1u);  // all ones for a Q-correlated entry
+#pragma unroll
+  for (int i = 0; i < F::ND; ++i) D[i] = c.nq[i] ^ ((q[i] ^ R ^ c.nq[i]) & qm);
+}
+
+// Stage table indices of a rank and the LDS reads.
+template <int NP>
+__device__ __forceinline__ void qba_closed_tables(uint32_t rank, const uint32_t *__restrict__ pl,
+                                                  uint4 &A, uint2 &sB, uint32_t &sC) {
+  using F = CF<NP>;
   uint32_t iA = 0, rem = rank;
   if constexpr (F::RA > 1) {
     const uint64_t pa = (uint64_t)rem * F::RA;
@@ -286,32 +312,30 @@ __device__ __forceinline__ void qba_closed_half(uint32_t w0, uint32_t w1, uint64
   }
   const uint64_t pb = (uint64_t)rem * F::RB;
   const uint32_t iB = (uint32_t)(pb >> 32);
+  const uint32_t iC = F::RC > 1 ? (uint32_t)(((uint64_t)(uint32_t)pb * F::RC) >> 32) : 0u;
 #ifdef QBA_EXP_NOTABLE
-  const uint4 A = make_uint4(iA, iA * 3u, iA * 5u, 0u);
-  const uint2 sB = make_uint2(iB, iB * 7u);
+  A = make_uint4(iA, iA * 3u, iA * 5u, 0u);
+  sB = make_uint2(iB, iB * 7u);
+  sC = iC * 9u;
 #else
-  const uint4 A = *reinterpret_cast<const uint4 *>(pl + 4 * iA);
-  const uint2 sB = *reinterpret_cast<const uint2 *>(pl + F::OFFB + 2 * iB);
+  A = *reinterpret_cast<const uint4 *>(pl + 4 * iA);
+  sB = *reinterpret_cast<const uint2 *>(pl + F::OFFB + 2 * iB);
+  sC = F::RC > 1 ? pl[F::OFFC + iC] : 0u;
 #endif
-  uint32_t q[4] = {A.x, A.y, A.z, A.w};
-  uint32_t y0 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.x), y1 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.y);
-  if constexpr (F::RC > 1) {
-    const uint32_t iC = (uint32_t)(((uint64_t)(uint32_t)pb * F::RC) >> 32);
-#ifdef QBA_EXP_NOTABLE
-    const uint2 sC = make_uint2(iC, iC * 9u);
-#else
-    const uint2 sC = *reinterpret_cast<const uint2 *>(pl + F::OFFC + 2 * iC);
-#endif
-    const uint32_t z0 = qba_perm_b(y1, y0, sC.x), z1 = qba_perm_b(y1, y0, sC.y);
-    y0 = z0;
-    y1 = z1;
-  }
-  q[F::WIN] = y0;
-  q[F::WIN + 1] = y1;
-  const uint32_t R = ((w0 >> 1) & (uint32_t)(QCfg<NP>::W - 1)) * 0x01010101u;
-  const bool isq = w0 & 1u;
-#pragma unroll
-  for (int i = 0; i < F::ND; ++i) D[i] = isq ? (q[i] ^ R) : nq[i];
+}
+
+template <int NP>
+__device__ __forceinline__ void qba_closed_half(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
+                                                uint32_t k0, uint32_t k1,
+                                                const uint32_t *__restrict__ pl,
+                                                uint32_t (&D)[CF<NP>::ND]) {
+  QbaClosed c;
+  qba_closed_rank<NP>(w0, w1, p, h, k0, k1, c);
+  uint4 A;
+  uint2 sB;
+  uint32_t sC;
+  qba_closed_tables<NP>(c.rank, pl, A, sB, sC);
+  qba_closed_finish<NP>(c, A, sB, sC, D);
 }
 
 // Entry e on its own (odd pair alignment, tails): the half of its pair's block.
@@ -488,13 +512,21 @@ __device__ __forceinline__ void qba_quad(uint32_t c0, uint32_t count, uint64_t f
     if constexpr (SAMP == QBA_S_CLOSED && !TAIL) {
       if (!(first & 1)) {  // wave-uniform: the quad is two whole pairs
         const uint64_t p0 = (first + c0) >> 1;
+        QbaClosed cl[4];
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) {
           const uint64_t p = p0 + jp;
           const QbaU4 x = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0u, 0u, k0, k1);
-          qba_closed_half<NP>(x.x, x.y, p, 0u, k0, k1, pl, D[2 * jp]);
-          qba_closed_half<NP>(x.z, x.w, p, 1u, k0, k1, pl, D[2 * jp + 1]);
+          qba_closed_rank<NP>(x.x, x.y, p, 0u, k0, k1, cl[2 * jp]);
+          qba_closed_rank<NP>(x.z, x.w, p, 1u, k0, k1, cl[2 * jp + 1]);
         }
+        uint4 A[4];
+        uint2 sB[4];
+        uint32_t sC[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qba_closed_tables<NP>(cl[j].rank, pl, A[j], sB[j], sC[j]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qba_closed_finish<NP>(cl[j], A[j], sB[j], sC[j], D[j]);
         done = true;
       }
     }

@@ -197,8 +197,9 @@ static bool q_closed(const QbaHostProgram &hp, int n) {
 //      those swaps, 4 words per entry (bytes 0..11, word 3 unused);
 //   window: the 8 bytes that hold the remaining positions (bytes 4..11 when
 //      n >= 8, else bytes 0..7 with positions 1..n);
-//   B: the first (up to) four window digits, C: the rest -> v_perm_b32
-//      selectors {lo, hi} of the window (out byte b = in byte sel[b]).
+//   B: the first (up to) four window digits -> v_perm_b32 selectors {lo, hi}
+//      of the window (out byte b = in byte sel[b]); C: the rest, whose swaps
+//      stay inside window bytes 4..7 -> the hi selector only.
 // Index of a stage = its digits in mixed radix, first digit most significant;
 // the three stage indices are the mixed-radix digits (A, B, C) of the rank.
 static void build_perm_tables(int n, std::vector<uint32_t> &words, uint32_t &ra, uint32_t &rb,
@@ -232,7 +233,7 @@ static void build_perm_tables(int n, std::vector<uint32_t> &words, uint32_t &ra,
       words.push_back((uint32_t)arr[4 * w] | (uint32_t)arr[4 * w + 1] << 8 |
                       (uint32_t)arr[4 * w + 2] << 16 | (uint32_t)arr[4 * w + 3] << 24);
   }
-  auto stage = [&](const std::vector<int> &rad, int first) {
+  auto stage = [&](const std::vector<int> &rad, int first, bool hi_only) {
     const uint32_t R = prod(rad);
     for (uint32_t idx = 0; idx < R; ++idx) {
       int sel[8];
@@ -245,16 +246,23 @@ static void build_perm_tables(int n, std::vector<uint32_t> &words, uint32_t &ra,
         const int i = first + (int)t;
         std::swap(sel[pos[i]], sel[pos[i + d]]);
       }
-      words.push_back((uint32_t)sel[0] | (uint32_t)sel[1] << 8 | (uint32_t)sel[2] << 16 |
-                      (uint32_t)sel[3] << 24);
+      if (!hi_only)
+        words.push_back((uint32_t)sel[0] | (uint32_t)sel[1] << 8 | (uint32_t)sel[2] << 16 |
+                        (uint32_t)sel[3] << 24);
       words.push_back((uint32_t)sel[4] | (uint32_t)sel[5] << 8 | (uint32_t)sel[6] << 16 |
                       (uint32_t)sel[7] << 24);
     }
   };
   offB = (int)words.size();
-  stage(radB, 0);
+  stage(radB, 0, false);
   offC = (int)words.size();
-  stage(radC, (int)radB.size());
+  // C's swaps all lie in window bytes 4..7 (its first position is the
+  // window's fifth): its lo selector is the identity and is not stored.
+  if (!radC.empty() && pos[radB.size()] < 4) {  // never: B takes the first four positions
+    words.clear();
+    return;
+  }
+  stage(radC, (int)radB.size(), true);
 }
 
 extern "C" int qba_resource_compile(qba_ctx *ctx, int n, int kind, const int32_t *gates, int ngates,
