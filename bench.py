@@ -1,21 +1,38 @@
 #!/usr/bin/env python3
 """Headline benchmark: list entries sampled+verified per second at n = 11.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-One step = one pass of the hot path over this rank's shard of sizeL: every
-entry is Born-sampled from the compiled resource program (Philox keyed by the
-global entry index), its n+1 list bytes are written to HBM, and the count-mode
-checks (isQCorr, P_u, every party's tuple histogram and every pairwise
-collision, the inputs of consistent()) are accumulated -- then, for N > 1, the
-count histograms are summed over ranks with one RCCL all-reduce.
+One step (default, --config 2) = one pass of the hot path over this rank's
+shard of sizeL: every entry is Born-sampled from the compiled resource program
+(Philox keyed by the global entry index), its n+1 list bytes are written to
+HBM, and the count-mode checks (isQCorr, P_u, every party's tuple histogram
+and every pairwise collision -- the inputs of consistent()) are accumulated;
+for N > 1 the count histograms are then summed over ranks with one RCCL
+all-reduce.
 
 Workload (config.workload): BASELINE.json configs[2] -- n = 11 parties,
 3 dishonest, sizeL = 1e9 sharded over 8 GPUs -- i.e. 1.25e8 entries per GPU.
 At N GPUs each rank owns 1.25e8 entries (weak scaling; N = 8 is exactly
-sizeL = 1e9).  configs[1] (sizeL = 1e6 on one GPU, 12 MB of lists) is
-cache-resident and launch-bound and is covered by the parity tests.
+sizeL = 1e9).  The metric is a node figure, so the node configuration sets
+the per-GPU shard; configs[1] (sizeL = 1e6, 12 MB of lists: cache-resident and
+launch-bound) is --config 1.
+
+Other BASELINE.json configs (one JSON line each, one GPU):
+  --config 0  configs[0]: n=3, nDis=1, sizeL=1000 protocol run (the
+              reference's CPU case) on the exact-mode host; CPU baseline = the
+              same host on the numpy oracle.
+  --config 1  configs[1]: n=11, sizeL=1e6, K steps captured in one hipGraph.
+  --config 3  configs[3]: 4096 independent n=7 instances x sizeL=1e5.
+  --config 4  configs[4]: the largest resource register in fp64 HBM (GHZ
+              register of the Q circuit, n+1 qubits); gate-pass GB/s.
+
+roofline.achieved = algorithmic bytes per launch (2(n+1) B per
+entry, lists written once + read once for verification, scored at that even
+though the fused kernel never re-reads them) / the launch's device time,
+measured with HIP events on the stream the kernels run on.  The launch is the
+whole sample_check call: the fused kernel and the slab reduction (qba_k_reduce).
 """
 from __future__ import annotations
 
@@ -33,6 +50,7 @@ PKG = "tfg---quantum-byzantine-agreement_amd"
 
 METRIC = "list entries sampled+verified/sec (node) at n=11; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s measured copy
+DATA = "synthetic: lists Born-sampled on the device (Philox4x32-10 keyed by entry index); no dataset"
 
 
 def parse():
@@ -40,6 +58,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=[0, 1, 2, 3, 4])
     ap.add_argument("--n", type=int, default=11)
     ap.add_argument("--dishonest", type=int, default=3)
     ap.add_argument("--per-gpu", type=float, default=1.25e8, help="entries per GPU per step")
@@ -47,30 +66,37 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sv-qubits", type=int, default=None, help="--config 4 register size")
     ap.add_argument("--traffic", default=str(ROOT / "profiles" / "traffic_n11.json"),
                     help="PMC-derived HBM bytes per launch (profiles/), if present")
     return ap.parse_args()
 
 
-def cpu_baseline(n, seed, info, target_s):
-    """The oracle's C twin (OpenMP, all host threads) on a bounded sample."""
+# ---------------------------------------------------------------------------
+# CPU baselines (the only place bench.py touches oracle/)
+# ---------------------------------------------------------------------------
+def cpu_baseline_counts(n, seed, info, target_s):
+    """The oracle's C twin (same schedule, same counts; OpenMP on every host
+    thread it is given) over a bounded sample, in 2^25-entry chunks."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle_lib
-    sample = 1 << 18
-    t0 = time.perf_counter()
-    oracle_lib.sample_counts(n, seed, 0, sample, info["notq"], info["q"], info["closed"])
-    dt = time.perf_counter() - t0
-    sample = int(min(max(sample, sample * target_s / max(dt, 1e-6)), 1 << 27))
-    t0 = time.perf_counter()
-    oracle_lib.sample_counts(n, seed, 0, sample, info["notq"], info["q"], info["closed"])
-    dt = time.perf_counter() - t0
-    return {"value": sample / dt, "unit": "entries/s", "cores": oracle_lib.threads(), "kind": "port",
-            "sample": f"{sample} entries of the same n={n} workload: C twin (oracle/sampler_ref.c) "
-                      f"sample + count, {dt:.2f} s"}
+    chunk = 1 << 25
+    done, t0 = 0, time.perf_counter()
+    while True:
+        oracle_lib.sample_counts(n, seed, done, chunk, info["notq"], info["q"], info["closed"])
+        done += chunk
+        dt = time.perf_counter() - t0
+        if dt >= target_s or done >= 1 << 32:
+            break
+    return {"value": done / dt, "unit": "entries/s", "cores": oracle_lib.threads(), "kind": "port",
+            "sample": f"{done} entries (entries [0, {done})) of the same n={n} workload: C twin "
+                      f"(oracle/sampler_ref.c) sample + count, {dt:.1f} s"}
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------------------
+# configs[2]: the headline (default)
+# ---------------------------------------------------------------------------
+def headline(args):
     import torch
     dist_mod = importlib.import_module(f"{PKG}.distributed")
     eng_mod = importlib.import_module(f"{PKG}.engine")
@@ -90,16 +116,16 @@ def main():
     counts = eng_mod.Counts(H, C, P)
     stream = torch.cuda.current_stream()
 
-    def step():
+    def launch():
         if args.mode == "fused":
             eng.sample_check(n, args.seed, first, per, lists, counts)
         else:
             eng.sample(n, args.seed, first, per, lists)
             eng.check_counts(lists, n, per, counts)
-        dist_mod.allreduce_counts(flat)
 
     for _ in range(args.warmup):
-        step()
+        launch()
+        dist_mod.allreduce_counts(flat)
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -109,11 +135,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        if args.mode == "fused":
-            eng.sample_check(n, args.seed, first, per, lists, counts)
-        else:
-            eng.sample(n, args.seed, first, per, lists)
-            eng.check_counts(lists, n, per, counts)
+        launch()
         ev[i][1].record(stream)
         dist_mod.allreduce_counts(flat)
     torch.cuda.synchronize()
@@ -130,6 +152,7 @@ def main():
     Hn, Cn, Pn = (x.cpu().numpy() for x in (H, C, P))
     offdiag = int(Cn.sum() - sum(Cn[:, g, g].sum() for g in range(n + 1)))
     if rank != 0:
+        eng.close()
         return
     entries = per * world * args.steps
     value = entries / t_max
@@ -153,25 +176,191 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic: lists Born-sampled on the device (Philox4x32-10 keyed by entry index); no dataset",
+        "data": DATA,
         "config": {
             "workload": f"BASELINE configs[2] shard: n={n} parties, {args.dishonest} dishonest, "
                         f"{per:.3g} entries/GPU (sizeL={per * world:.3g} over {world} GPU)",
             "n_parties": n, "n_dishonest": args.dishonest, "entries_per_gpu": per,
-            "sizeL": per * world, "mode": args.mode,
+            "sizeL": per * world, "mode": args.mode, "sampler": "closed" if info["closed"] else "tables",
             "parallelism": f"sizeL sharded over {world} GPU(s), RCCL all-reduce of counts",
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "qba_k_lists<11,1> (+qba_k_reduce)" if args.mode == "fused" else "qba_k_lists<11,0>+<11,2>",
-            "algorithmic_bytes_per_entry": bytes_per_entry, "kernel_ms": kern_ms,
+            "kernel": f"qba_k_lists<{n},1,*> + qba_k_reduce" if args.mode == "fused"
+                      else f"qba_k_lists<{n},0,*> + qba_k_lists<{n},2,*> + reduce",
+            "algorithmic_bytes_per_entry": bytes_per_entry, "launch_ms": kern_ms,
         },
         "verification": {"q_entries": int(Pn.sum()), "offdiag_collisions": offdiag},
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(n, args.seed, info, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline_counts(n, args.seed, info, args.cpu_seconds)
     print(json.dumps(out), flush=True)
+    eng.close()
+
+
+# ---------------------------------------------------------------------------
+# the other configs (one GPU)
+# ---------------------------------------------------------------------------
+def _line(args, value, unit, workload, roofline, extra=None, higher=True, dtype="u8"):
+    out = {"metric": METRIC, "value": value, "unit": unit, "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "higher_is_better": higher, "scaling": "weak", "vs_baseline": None,
+           "dtype": dtype, "data": DATA, "config": {"workload": workload, "parallelism": "1 GPU"},
+           "roofline": roofline}
+    out.update(extra or {})
+    return out
+
+
+def config0(args, eng):
+    """configs[0]: mpiexec -n 4 python tfg.py 1000 1 -> the tfg.py-compatible
+    host's in-process world, exact-order checks on the GPU engine."""
+    protocol = importlib.import_module(f"{PKG}.protocol")
+    runs = []
+    protocol.run_local(3, 1000, 1, eng, seed=1)  # warm (compiles n=3)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        runs.append(protocol.run_local(3, 1000, 1, eng, seed=1 + s))
+    dt = (time.perf_counter() - t0) / args.steps
+    extra = {"ms_per_step": dt * 1e3,
+             "protocol": {"success": [r.result["success"] for r in runs[:5]],
+                          "messages": runs[0].messages, "bytes": runs[0].bytes}}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        sys.path.insert(0, str(ROOT / "tests"))
+        from oracle_engine import OracleEngine  # numpy restatement (test infrastructure)
+        import numpy as np
+        import tfg_oracle as orc
+        oe = OracleEngine()
+        lists = [orc.closed_form_lists(3, 1000, np.random.default_rng(s)) for s in range(args.steps)]
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            protocol.run_local(3, 1000, 1, oe, seed=1 + s, lists=lists[s])
+        cdt = (time.perf_counter() - t0) / args.steps
+        extra["cpu_baseline"] = {"value": 1000 / cdt, "unit": "entries/s", "cores": 1, "kind": "port",
+                                 "sample": f"{args.steps} protocol runs, numpy oracle engine in place of "
+                                           f"the GPU engine (lists drawn on the host)"}
+    return _line(args, 1000 / dt, "entries/s (whole protocol run, sizeL=1000)",
+                 "BASELINE configs[0]: n=3 parties, 1 dishonest, sizeL=1000, protocol rounds "
+                 "(in-process mpiexec world)",
+                 {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None,
+                  "traffic": None, "note": "host protocol rounds; per-packet device calls"}, extra)
+
+
+def config1(args, eng):
+    """configs[1]: n=11, sizeL=1e6 on one GPU; K steps in one hipGraph."""
+    import torch
+    n, count = 11, 1_000_000
+    info = eng.prepare(n)
+    lists = eng.alloc_lists(n, count)
+    counts = eng.alloc_counts(n)
+    eng.sample_check(n, args.seed, 0, count, lists, counts)  # allocates scratch before capture
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(args.steps):
+                eng.sample_check(n, args.seed, 0, count, lists, counts)
+    torch.cuda.synchronize()
+    for _ in range(max(1, args.warmup)):
+        g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    t0 = time.perf_counter()
+    g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / args.steps
+    dev = a.elapsed_time(b) * 1e-3 / args.steps
+    ach = 24 * count / dev / 1e9
+    extra = {"ms_per_step": wall * 1e3}
+    if not args.no_cpu_baseline:
+        extra["cpu_baseline"] = cpu_baseline_counts(n, args.seed, info, args.cpu_seconds / 2)
+    return _line(args, count / wall, "entries/s",
+                 "BASELINE configs[1]: n=11 parties, 3 dishonest, sizeL=1e6 on one GPU "
+                 f"({args.steps} steps in one hipGraph)",
+                 {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                  "note": "12 MB of lists stay in the 256 MB Infinity Cache; launch-bound"}, extra)
+
+
+def config3(args, eng, n_inst=4096, count=100_000):
+    """configs[3]: 4096 independent 7-party instances x sizeL=1e5 per GPU."""
+    import torch
+    n = 7
+    lists, c = eng.sample_check_batched(n, args.seed, n_inst, count)
+    for _ in range(args.warmup):
+        eng.sample_check_batched(n, args.seed, n_inst, count, lists)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    a.record()
+    for _ in range(args.steps):
+        lists, c = eng.sample_check_batched(n, args.seed, n_inst, count, lists)
+    b.record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / args.steps
+    dev = a.elapsed_time(b) * 1e-3 / args.steps
+    ent = n_inst * count
+    ach = 16 * ent / dev / 1e9
+    honest = bool((c.C.sum((1, 2, 3)) == c.P.sum(1) * (n + 1)).all().item())
+    extra = {"ms_per_step": wall * 1e3, "verification": {"all_instances_collision_free": honest}}
+    return _line(args, ent / wall, "entries/s",
+                 f"BASELINE configs[3]: {n_inst} independent n=7 instances x sizeL={count} per GPU",
+                 {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": ach / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_entry": 16}, extra)
+
+
+def config4(args, eng):
+    """configs[4]: the largest resource register whose fp64 statevector fits HBM."""
+    import numpy as np
+    import torch
+    free, _ = torch.cuda.mem_get_info()
+    q = args.sv_qubits
+    if q is None:
+        q = 1
+        while (8 << (q + 1)) < free * 0.95:
+            q += 1
+    sv = torch.empty(1 << q, dtype=torch.float64, device=eng.device)
+    gates = np.array([(0, 0, -1)] + [(1, t, 0) for t in range(1, q)], np.int32)  # GHZ register
+    eng.statevector(q, gates[:1], out=sv)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    eng.apply_gates(sv, q, gates[1:])
+    b.record()
+    torch.cuda.synchronize()
+    t = a.elapsed_time(b) * 1e-3
+    idx, prob = eng.support(sv, q, cap=16)
+    passes = q - 1  # CX passes: each swaps the control = 1 half, 8 B read + 8 B written per pair member
+    gbs = passes * 8 * (1 << q) / t / 1e9
+    ok = len(idx) == 2 and abs(prob[0] - 0.5) < 1e-12 and abs(prob[1] - 0.5) < 1e-12
+    return _line(args, gbs, "GB/s (gate passes)",
+                 f"BASELINE configs[4]: GHZ register of the Q resource, {q} qubits fp64 "
+                 f"(n={q - 1} parties), {(8 << q) / 2 ** 30:.0f} GiB",
+                 {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                  "algorithmic_bytes_per_amplitude_pass": 8,
+                  "note": "CX pass: the control = 1 half of the register is read and written once"},
+                 {"ms_per_step": t / passes * 1e3,
+                  "verification": {"support": [int(i) for i in idx], "probs": [float(p) for p in prob],
+                                   "ghz_exact": bool(ok)}}, dtype="f64")
+
+
+def main():
+    args = parse()
+    if args.config == 2:
+        headline(args)
+        return
+    if args.gpus != 1 or int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--config 0/1/3/4 are single-GPU measurements")
+    import torch
+    torch.cuda.set_device(0)
+    eng = importlib.import_module(f"{PKG}.engine").Engine(0)
+    fn = {0: config0, 1: config1, 3: config3, 4: config4}[args.config]
+    print(json.dumps(fn(args, eng)), flush=True)
     eng.close()
 
 

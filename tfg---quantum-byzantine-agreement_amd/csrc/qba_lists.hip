@@ -35,6 +35,7 @@ struct QCfg {
   static constexpr int CBL = W * CP;
   static constexpr int STATS = 2;  // [0] Q entries with a value >= W (invalid), [1] spare
   static constexpr int NBINS = HBL + CBL + STATS;
+  static constexpr int NBP = (NBINS + 3) & ~3;  // slab row stride (16-B rows)
   // counted index of the pair g < h
   __host__ __device__ static constexpr int pidx(int g, int h) { return g * (2 * G - g - 1) / 2 + (h - g - 1); }
   __host__ __device__ static constexpr int hidx(int u, int g, int x) { return (u * G + g) * WP + x; }
@@ -586,7 +587,7 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
     for (int i = threadIdx.x; i < ntab; i += BS) lds[i] = tab[i];
     apat = lds + T;
     thr = lds + 2 * T;
-    hist = reinterpret_cast<uint32_t *>(lds + ntab);
+    hist = reinterpret_cast<uint32_t *>(lds + ((ntab + 1) & ~1));  // 16-B aligned
   }
   return hist;
 }
@@ -603,7 +604,7 @@ __global__ void __launch_bounds__(QBA_LBLOCK)
   const uint32_t *pl;
   uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
   if (MODE != 0)
-    for (int i = threadIdx.x; i < C::NBINS; i += BS) hist[i] = 0u;
+    for (int i = threadIdx.x; i < C::NBP; i += BS) hist[i] = 0u;
   __syncthreads();
   const uint32_t nfull = count >> 2;
   for (uint32_t q = blockIdx.x * BS + threadIdx.x; q < nfull; q += gridDim.x * BS)
@@ -613,8 +614,9 @@ __global__ void __launch_bounds__(QBA_LBLOCK)
                                    ld, hist);
   if (MODE != 0) {
     __syncthreads();
-    uint32_t *dst = slab + (size_t)blockIdx.x * C::NBINS;
-    for (int i = threadIdx.x; i < C::NBINS; i += BS) dst[i] = hist[i];
+    uint4 *dst = reinterpret_cast<uint4 *>(slab + (size_t)blockIdx.x * C::NBP);
+    const uint4 *src = reinterpret_cast<const uint4 *>(hist);
+    for (int i = threadIdx.x; i < C::NBP / 4; i += BS) dst[i] = src[i];
   }
 }
 
@@ -659,57 +661,65 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   }
 }
 
-// Column sums of the slab: workgroup (x, y) sums rows [y*R, (y+1)*R) of 256
-// bins and adds the partial into acc (integer atomics: order-independent, so
-// the result is bitwise reproducible).
+// Slab reduction.  Workgroup (x, y) sums slab rows [y*RP, (y+1)*RP) for 1024
+// bins (4 per thread, 16-B loads) and adds its partial into the u64
+// accumulator with integer atomics (order-independent: bitwise reproducible).
+#define QBA_RED_ROWS 32
 template <int NP>
 __global__ void __launch_bounds__(256)
-    qba_k_reduce_cols(const uint32_t *__restrict__ slab, int nblocks, int rows_per,
-                      unsigned long long *__restrict__ acc) {
+    qba_k_reduce(const uint32_t *__restrict__ slab, int nrows, unsigned long long *__restrict__ acc) {
   using C = QCfg<NP>;
-  const int bin = blockIdx.x * 256 + threadIdx.x;
-  if (bin >= C::NBINS) return;
-  const int b0 = blockIdx.y * rows_per;
-  const int b1 = b0 + rows_per < nblocks ? b0 + rows_per : nblocks;
-  unsigned long long s = 0;
-  for (int b = b0; b < b1; ++b) s += slab[(size_t)b * C::NBINS + bin];
-  if (s) atomicAdd(&acc[bin], s);
+  const int q = blockIdx.x * 256 + threadIdx.x;  // bin quad
+  if (4 * q >= C::NBP) return;
+  const int b0 = blockIdx.y * QBA_RED_ROWS;
+  const int b1 = b0 + QBA_RED_ROWS < nrows ? b0 + QBA_RED_ROWS : nrows;
+  unsigned long long s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll 8
+  for (int b = b0; b < b1; ++b) {
+    const uint4 v = reinterpret_cast<const uint4 *>(slab + (size_t)b * C::NBP)[q];
+    s0 += v.x;
+    s1 += v.y;
+    s2 += v.z;
+    s3 += v.w;
+  }
+  if (s0) atomicAdd(&acc[4 * q], s0);
+  if (s1) atomicAdd(&acc[4 * q + 1], s1);
+  if (s2) atomicAdd(&acc[4 * q + 2], s2);
+  if (s3) atomicAdd(&acc[4 * q + 3], s3);
 }
 
-// acc -> the int64 outputs (see qba.h for shapes): H as is, C symmetrised
-// with |P_u| on the diagonal, P[u] = |P_u| = H[u][1][u].
+// acc -> the int64 outputs (see qba.h for shapes): H as is (group 1's bins
+// derived, see qba_psize), C symmetrised with |P_u| on the diagonal, P, the
+// stats.  One workgroup: it stages the accumulator in LDS, zeroes it for the
+// next reduction (so no memset precedes one) and writes from the copy.
 template <int NP>
-__global__ void __launch_bounds__(256)
-    qba_k_finalize(const unsigned long long *__restrict__ acc, int64_t *__restrict__ H,
+__global__ void __launch_bounds__(1024)
+    qba_k_finalize(unsigned long long *__restrict__ acc, int64_t *__restrict__ H,
                    int64_t *__restrict__ Cc, int64_t *__restrict__ P, int64_t *__restrict__ stats,
                    int accumulate, int stats_accumulate) {
   using C = QCfg<NP>;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  auto put = [&](int64_t *dst, int64_t v) { *dst = accumulate ? *dst + v : v; };
-  if (i < C::HB) {
-    put(&H[i], qba_hval<NP>(acc, i));
-    return;
+  __shared__ unsigned long long a[C::NBP];
+  for (int i = threadIdx.x; i < C::NBP; i += 1024) {
+    a[i] = acc[i];
+    acc[i] = 0ull;
   }
-  int r = i - C::HB;
-  if (r < C::CB) {
+  __syncthreads();
+  auto put = [&](int64_t *dst, int64_t v) { *dst = accumulate ? *dst + v : v; };
+  for (int i = threadIdx.x; i < C::HB; i += 1024) put(&H[i], qba_hval<NP>(a, i));
+  for (int r = threadIdx.x; r < C::CB; r += 1024) {
     const int u = r / (C::G * C::G), g = (r / C::G) % C::G, h = r % C::G;
     if (g < h) {
-      const int64_t v = (int64_t)acc[C::HBL + u * C::CP + C::pidx(g, h)];
+      const int64_t v = (int64_t)a[C::HBL + u * C::CP + C::pidx(g, h)];
       put(&Cc[r], v);
       put(&Cc[(u * C::G + h) * C::G + g], v);
     } else if (g == h) {
-      put(&Cc[r], qba_psize<NP>(acc, u));
+      put(&Cc[r], qba_psize<NP>(a, u));
     }
-    return;
   }
-  r -= C::CB;
-  if (r < C::W) {
-    put(&P[r], qba_psize<NP>(acc, r));
-    return;
-  }
-  r -= C::W;
-  if (r < C::STATS && stats)
-    stats[r] = (stats_accumulate ? stats[r] : 0) + (int64_t)acc[C::HBL + C::CBL + r];
+  if (threadIdx.x < C::W) put(&P[threadIdx.x], qba_psize<NP>(a, threadIdx.x));
+  if (threadIdx.x < C::STATS && stats)
+    stats[threadIdx.x] = (stats_accumulate ? stats[threadIdx.x] : 0) +
+                         (int64_t)a[C::HBL + C::CBL + threadIdx.x];
 }
 
 // ---------------------------------------------------------------------------
@@ -728,9 +738,9 @@ struct QbaLaunch {
   int stats_accumulate;
 };
 
-static int nbins_of(int n) {
+static int nbins_of(int n) {  // QCfg<n>::NBP
   const int g = n + 1, q = qba_nq(n), w = 1 << q;
-  return w * g * (w + 1) + w * g * (g - 1) / 2 + 2;
+  return (w * g * (w + 1) + w * g * (g - 1) / 2 + 2 + 3) & ~3;
 }
 
 // Persistent grid: every resident workgroup slot of the chip (LDS- and
@@ -741,7 +751,7 @@ static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count) 
       per_cu < 1)
     per_cu = 1;
   const uint64_t nquad = (count + 3) >> 2;
-  uint64_t g = (nquad + QBA_LBLOCK - 1) / QBA_LBLOCK;
+  uint64_t g = (nquad + 2 * QBA_LBLOCK - 1) / (2 * QBA_LBLOCK);  // >= 2 quads per thread
   const uint64_t cap = (uint64_t)ctx->num_cus * (uint64_t)per_cu;
   if (g > cap) g = cap;
   if (g < 1) g = 1;
@@ -760,7 +770,7 @@ static int sampler_of(const QbaProgramSet *hs) {
 template <int NP>
 static size_t table_lds(const QbaProgramSet *hs, int samp) {
   if (samp == QBA_S_CLOSED) return (size_t)((CF<NP>::WORDS + 3) & ~3) * sizeof(uint32_t);
-  return (size_t)(hs->any_nonuniform ? 3 : 1) * hs->table_total * sizeof(uint64_t);
+  return (size_t)(((hs->any_nonuniform ? 3 : 1) * hs->table_total + 1) & ~1) * sizeof(uint64_t);
 }
 
 template <int NP>
@@ -782,7 +792,7 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
     if (int rc = check_closed<NP>(hs)) return rc;
     lds += table_lds<NP>(hs, samp);
   }
-  if (L.mode != 0) lds += (size_t)C::NBINS * sizeof(uint32_t);
+  if (L.mode != 0) lds += (size_t)C::NBP * sizeof(uint32_t);
   lds = (lds + 15) & ~(size_t)15;
   if (lds == 0) lds = 16;
   const void *kern = nullptr;
@@ -804,7 +814,7 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
   const int grid = grid_for(ctx, kern, lds, L.count);
   uint32_t *slab = nullptr;
   if (L.mode != 0) {
-    int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBINS * sizeof(uint32_t));
+    int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBP * sizeof(uint32_t));
     if (rc) return rc;
     slab = reinterpret_cast<uint32_t *>(ctx->slab);
   }
@@ -820,14 +830,11 @@ static int launch_np(qba_ctx *ctx, const QbaLaunch &L) {
   int rc = QBA_OK;
   if (rc || L.mode == 0) return rc;
   unsigned long long *acc = reinterpret_cast<unsigned long long *>(ctx->acc);
-  QBA_HIP(hipMemsetAsync(acc, 0, sizeof(unsigned long long) * C::NBINS, L.stream));
-  const int rows_per = 32;
-  hipLaunchKernelGGL(qba_k_reduce_cols<NP>, dim3((C::NBINS + 255) / 256, (grid + rows_per - 1) / rows_per),
-                     dim3(256), 0, L.stream, slab, grid, rows_per, acc);
+  const dim3 rgrid((C::NBP / 4 + 255) / 256, (grid + QBA_RED_ROWS - 1) / QBA_RED_ROWS);
+  hipLaunchKernelGGL(qba_k_reduce<NP>, rgrid, dim3(256), 0, L.stream, slab, grid, acc);
   QBA_HIP(hipGetLastError());
-  const int items = C::HB + C::CB + C::W + C::STATS;
-  hipLaunchKernelGGL(qba_k_finalize<NP>, dim3((items + 255) / 256), dim3(256), 0, L.stream, acc,
-                     L.H, L.C, L.P, L.stats, L.accumulate, L.stats_accumulate);
+  hipLaunchKernelGGL(qba_k_finalize<NP>, dim3(1), dim3(1024), 0, L.stream, acc, L.H, L.C, L.P,
+                     L.stats, L.accumulate, L.stats_accumulate);
   QBA_HIP(hipGetLastError());
   return QBA_OK;
 }
