@@ -1,0 +1,36 @@
+// qba_lists.h -- interface between the list-kernel dispatch (qba_lists.hip)
+// and the per-n kernel instantiations (qba_lists_inst.hip, one object per n:
+// the templates in qba_lists_kern.h are compiled 15 times in parallel).
+#pragma once
+
+#include "qba_internal.h"
+
+struct QbaLaunch {
+  int n;
+  int mode;
+  const QbaProgramSet *ps;
+  uint64_t seed, first, count;
+  uint8_t *lists;
+  uint64_t ld;
+  int64_t *H, *C, *P, *stats;
+  int accumulate;
+  hipStream_t stream;
+  int stats_accumulate;
+};
+
+struct QbaBatch {
+  int n;
+  const QbaProgramSet *ps;
+  uint64_t seed_base;
+  int64_t n_inst;
+  uint64_t count;
+  uint8_t *lists;
+  uint64_t ld, inst_stride;
+  int64_t *H, *C, *P;
+  hipStream_t stream;
+};
+
+template <int NP>
+int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L);
+template <int NP>
+int qba_launch_batched(qba_ctx *ctx, const QbaBatch &B);

@@ -1,0 +1,905 @@
+// qba_lists_kern.h -- the data-parallel hot path on gfx950 (kernels and their
+// per-n launchers; instantiated by qba_lists_inst.hip):
+//   * Born sampling of list entries (tfg.py:68-84 + 128-129) from the compiled
+//     factored alias-table program, Philox4x32-10 keyed by the global entry;
+//   * the count-mode check pass (tfg.py:87-98, 182, 189, 291-294, 327):
+//     per Q-correlated entry, H[u][g][x] += 1 for every group g and
+//     C[u][g][h] += 1 for every equal pair, u = L1[k];
+//   * the fused sample+check kernel that writes each list byte once and
+//     counts from registers.
+//
+// Layout: lists[g][k] uint8, row stride ld (SoA: a party's list is one row).
+// A thread owns 4 consecutive entries (one dword per row), so every row store
+// / load of a wave is 256 contiguous bytes.  Histograms are privatised per
+// workgroup in LDS and flushed as u32 partials to a slab that a second
+// kernel reduces into int64 (bitwise reproducible, no global atomics).
+#pragma once
+#include <type_traits>
+
+#include "qba_lists.h"
+
+#ifndef QBA_WIDE_QPT  // quads per thread-step of the wide kernels (experiment builds: 4)
+#define QBA_WIDE_QPT 2
+#endif
+
+
+template <int NP>
+struct QCfg {
+  static constexpr int G = NP + 1;  // measured groups (n parties + the commander's extra)
+  static constexpr int NQ = (G <= 2) ? 1 : (G <= 4) ? 2 : (G <= 8) ? 3 : 4;
+  static constexpr int N = G * NQ;  // qubits of the circuit (tfg.py:44)
+  static constexpr int W = 1 << NQ;  // |W| (tfg.py:318)
+  static constexpr int HB = W * G * W;    // H as returned: [u][g][x]
+  static constexpr int WP = W + 1;        // LDS row stride of H: +1 word spreads banks
+  static constexpr int HBL = W * G * WP;  // H as counted in LDS / the slab
+  static constexpr int CB = W * G * G;      // C as returned: [u][g][h]
+  static constexpr int CP = G * (G - 1) / 2; // pairs g < h, as counted
+  static constexpr int CBL = W * CP;
+  static constexpr int STATS = 2;  // [0] Q entries with a value >= W (invalid), [1] spare
+  static constexpr int NBINS = HBL + CBL + STATS;
+  static constexpr int NBP = (NBINS + 3) & ~3;  // slab row stride (16-B rows)
+  // counted index of the pair g < h
+  __host__ __device__ static constexpr int pidx(int g, int h) { return g * (2 * G - g - 1) / 2 + (h - g - 1); }
+  __host__ __device__ static constexpr int hidx(int u, int g, int x) { return (u * G + g) * WP + x; }
+  // number of not-Q table bytes of the canonical program (ceil(n*nQ/8))
+  static constexpr int NFB = (NP * NQ + 7) / 8;
+  static constexpr int LASTB = NP * NQ - 8 * (NFB - 1);
+  using Out = typename std::conditional<(N <= 32), uint32_t, uint64_t>::type;
+  static constexpr Out M = (Out)(W - 1);
+  __host__ __device__ static constexpr int shift(int g) { return N - (g + 1) * NQ; }
+  __host__ __device__ static constexpr Out identity() {
+    Out p = 0;
+    for (int g = 1; g <= NP; ++g) p |= (Out)g << shift(g);
+    return p;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// random words of one entry (schedule documented in qba_internal.h)
+// ---------------------------------------------------------------------------
+// Words beyond block 0 (only programs with many or non-uniform factors):
+// kept out of line so the common path stays small.
+__device__ __attribute__((noinline)) uint32_t qba_word_ext(int kk, uint32_t elo, uint32_t ehi,
+                                                           uint32_t k0, uint32_t k1) {
+  const QbaU4 y = qba_philox(elo, ehi, 1u + (uint32_t)(kk >> 2), 0u, k0, k1);
+  const int s = kk & 3;
+  return s == 0 ? y.x : (s == 1 ? y.y : (s == 2 ? y.z : y.w));
+}
+
+// Word k of the table stream (k is wave-uniform).  Block-0 words are picked
+// with uniform masks so the selection stays in registers.
+__device__ __forceinline__ uint32_t qba_word(int kind, int k, const QbaU4 &x, uint32_t elo,
+                                             uint32_t ehi, uint32_t k0, uint32_t k1) {
+  k = __builtin_amdgcn_readfirstlane(k);
+  const int base = kind ? 1 : 3;
+  if (k >= base) return qba_word_ext(k - base, elo, ehi, k0, k1);
+  const uint32_t m0 = k == 0 ? ~0u : 0u, m1 = k == 1 ? ~0u : 0u, m2 = k == 2 ? ~0u : 0u;
+  return (x.y & m0) | (x.z & m1) | (x.w & m2);
+}
+
+template <typename Out>
+__device__ __forceinline__ Out qba_draw(const QbaProgram &P, int kind, const QbaU4 &x,
+                                        uint32_t elo, uint32_t ehi, uint32_t k0, uint32_t k1,
+                                        const uint64_t *pat, const uint64_t *apat,
+                                        const uint64_t *thr) {
+  Out out = 0;
+  const int nf = P.nfac;
+  for (int f = 0; f < nf; ++f) {
+    const QbaFactor F = P.fac[f];
+    const uint32_t wv = qba_word(kind, F.col_word, x, elo, ehi, k0, k1);
+    const uint32_t col = (wv >> F.col_shift) & ((1u << F.bits) - 1u);
+    uint64_t p = pat[F.offset + col];
+    if (!F.uniform) {
+      const uint32_t u = qba_word(kind, F.u_word, x, elo, ehi, k0, k1);
+      if ((uint64_t)u >= thr[F.offset + col]) p = apat[F.offset + col];
+    }
+    out ^= (Out)p;
+  }
+  return out;
+}
+
+// Uniform permutation pi of 1..n in the outcome layout (field g = pi(g)):
+// mixed-radix digits of floor(F * n! / 2^64) drive Fisher-Yates; Lemire's
+// test on the final fraction makes it exactly uniform.
+template <int NP>
+__device__ __forceinline__ bool qba_perm(uint64_t F, uint64_t t, typename QCfg<NP>::Out &mask) {
+  using C = QCfg<NP>;
+  using Out = typename C::Out;
+  Out P = C::identity();
+#pragma unroll
+  for (int i = NP; i >= 2; --i) {
+    const uint64_t lo = (F & 0xffffffffull) * (uint64_t)i;
+    const uint64_t hi = (F >> 32) * (uint64_t)i + (lo >> 32);
+    const uint32_t d = (uint32_t)(hi >> 32);
+    F = (hi << 32) | (lo & 0xffffffffull);
+    const int si = C::shift(i);
+    const int sj = C::N - (int)(d + 2) * C::NQ;  // field j = 1 + d
+    const Out a = (P >> si) & C::M;
+    const Out b = (P >> sj) & C::M;
+    const Out tt = a ^ b;
+    P ^= (tt << si) | (tt << sj);
+  }
+  mask = P;
+  return F >= t;
+}
+
+template <int NP>
+__device__ __forceinline__ typename QCfg<NP>::Out qba_sample_entry(
+    uint64_t e, uint32_t k0, uint32_t k1, const QbaProgramSet *__restrict__ ps,
+    const uint64_t *pat, const uint64_t *apat, const uint64_t *thr) {
+  using Out = typename QCfg<NP>::Out;
+  const uint32_t elo = (uint32_t)e, ehi = (uint32_t)(e >> 32);
+  const QbaU4 x = qba_philox(elo, ehi, 0u, 0u, k0, k1);
+  Out out;
+  if (x.x & 1u) {  // Q-correlated shot (tfg.py:69, 74)
+    const uint64_t t = ps->prog[1].perm_t;
+    Out mask;
+    bool ok = qba_perm<NP>((uint64_t)x.z | ((uint64_t)x.w << 32), t, mask);
+    for (uint32_t a = 1; !ok; ++a) {  // probability ~ n!/2^64 per entry
+      const QbaU4 y = qba_philox(elo, ehi, 0x80000000u + a, 0u, k0, k1);
+      ok = qba_perm<NP>((uint64_t)y.x | ((uint64_t)y.y << 32), t, mask);
+    }
+    out = qba_draw<Out>(ps->prog[1], 1, x, elo, ehi, k0, k1, pat, apat, thr) ^ mask;
+  } else {  // not-Q-correlated shot (tfg.py:72)
+    out = qba_draw<Out>(ps->prog[0], 0, x, elo, ehi, k0, k1, pat, apat, thr);
+  }
+  return out;
+}
+
+// Canonical programs (QbaProgramSet::canonical): every table column is a byte
+// of the stream, so the factor loop is fully unrolled at compile time.
+template <int NP>
+__device__ __forceinline__ typename QCfg<NP>::Out qba_sample_entry_fast(
+    uint64_t e, uint32_t k0, uint32_t k1, uint64_t perm_t, int qoff, const uint64_t *pat) {
+  using C = QCfg<NP>;
+  using Out = typename C::Out;
+  const uint32_t elo = (uint32_t)e, ehi = (uint32_t)(e >> 32);
+  const QbaU4 x = qba_philox(elo, ehi, 0u, 0u, k0, k1);
+  Out out;
+  if (x.x & 1u) {
+    Out mask;
+    bool ok = qba_perm<NP>((uint64_t)x.z | ((uint64_t)x.w << 32), perm_t, mask);
+    for (uint32_t a = 1; !ok; ++a) {
+      const QbaU4 y = qba_philox(elo, ehi, 0x80000000u + a, 0u, k0, k1);
+      ok = qba_perm<NP>((uint64_t)y.x | ((uint64_t)y.y << 32), perm_t, mask);
+    }
+    out = (Out)pat[qoff + (x.y & (uint32_t)C::M)] ^ mask;
+  } else {
+    out = 0;
+#pragma unroll
+    for (int f = 0; f < C::NFB; ++f) {
+      const uint32_t w = f < 4 ? x.y : (f < 8 ? x.z : x.w);
+      const uint32_t bits = f < C::NFB - 1 ? 8 : C::LASTB;
+      const uint32_t col = (w >> (8 * (f & 3))) & ((1u << bits) - 1u);
+      out ^= (Out)pat[256 * f + col];
+    }
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// Closed-form sampler (QbaProgramSet::closed; n <= 11).  Entries come in
+// pairs: entry e uses half h = e & 1 of block
+//   x = philox(ctr = {p_lo, p_hi, 0, 0}, key = seed),  p = e >> 1,
+// i.e. the 64 bits w0 = x[2h], w1 = x[2h+1].  isQ = w0 & 1.
+//   not-Q: values v_0..v_13 = the nQ low bits of the nibbles at bits
+//          {0,8,16,24, 4,12,20,28} of w1 then {8,16,24, 12,20,28} of w0;
+//          group g >= 1 takes v_{g-1}, group 0 takes v_0 (= group 1,
+//          tfg.py:15-22).
+//   Q:     r = (w0 >> 1) & (W-1).  The rank word F is w1 if
+//          F * n! mod 2^32 >= 2^32 mod n!, else w0 & ~31 (bits 5..31, a
+//          27-bit fraction) if F * n! mod 2^32 >= (2^27 mod n!) << 5 (Lemire on
+//          27 bits), else the words of philox(ctr = {p_lo, p_hi, 0x80000000 + a,
+//          h}) for a = 1, 2, ... in order (32-bit test): exactly uniform.
+//          (iA, iB, iC) = the mixed-radix digits of floor(F * n! / 2^32) in
+//          radices (RA, RB, RC) [F * RA = iA:F1, F1 * RB = iB:F2, F2 * RC =
+//          iC:F3], pi = stage A[iA] with its window permuted by B[iB] then
+//          C[iC]; group g = r ^ pi(g) (tfg.py:25-40).
+// Values are produced as bytes, group g in byte g % 4 of word g / 4.
+// ---------------------------------------------------------------------------
+// |P_u| = sum_x H[u][0][x]; H[u][1][x] = [x == u] |P_u| (group 1's own bin is
+// never counted: L1 = u by definition of the bin).
+template <int NP, typename T>
+__device__ __forceinline__ int64_t qba_psize(const T *bins, int u) {
+  using C = QCfg<NP>;
+  int64_t s = 0;
+  for (int x = 0; x < C::W; ++x) s += (int64_t)bins[C::hidx(u, 0, x)];
+  return s;
+}
+template <int NP, typename T>
+__device__ __forceinline__ int64_t qba_hval(const T *bins, int i) {  // i indexes H[u][g][x]
+  using C = QCfg<NP>;
+  const int u = i / (C::G * C::W), g = (i / C::W) % C::G, x = i % C::W;
+  if (g == 1) return x == u ? qba_psize<NP>(bins, u) : 0;
+  return (int64_t)bins[C::hidx(u, g, x)];
+}
+
+template <int NP>
+struct CF {
+  using C = QCfg<NP>;
+  static constexpr int G = NP + 1;
+  static constexpr int ND = (G + 3) / 4;          // words per entry
+  static constexpr int WIN = NP >= 8 ? 1 : 0;      // first word of the 8-byte window
+  static constexpr int K = NP >= 8 ? NP - 3 : NP;  // window positions that move
+  static constexpr uint32_t fact(int a, int b) {   // a * (a-1) * ... * b
+    uint32_t x = 1;
+    for (int i = a; i >= b; --i) x *= (uint32_t)i;
+    return x;
+  }
+  static constexpr uint32_t RA = NP >= 8 ? fact(NP, NP - 2) : 1u;
+  static constexpr uint32_t RB = K >= 2 ? fact(K, (K - 3 > 2 ? K - 3 : 2)) : 1u;
+  static constexpr uint32_t RC = K >= 6 ? fact(K - 4, 2) : 1u;
+  static constexpr uint32_t NFACT = fact(NP, 2);
+  static constexpr uint32_t T32 = (uint32_t)((1ull << 32) % NFACT);
+  static constexpr uint32_t T27 = (uint32_t)(((1ull << 27) % NFACT) << 5);  // 27-bit test, scaled
+  static constexpr int OFFB = 4 * (int)RA;            // in words
+  static constexpr int OFFC = OFFB + 2 * (int)RB;
+  static constexpr int WORDS = OFFC + (int)RC;  // C keeps only its hi selector
+  static constexpr uint32_t M4 = (uint32_t)(C::W - 1) * 0x01010101u;
+};
+
+__device__ __forceinline__ uint32_t qba_perm_b(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// Lemire acceptance of a 32-bit rank word against threshold T (scaled)
+template <int NP>
+__device__ __forceinline__ bool qba_accept(uint32_t F, uint32_t T) {
+  return F * CF<NP>::NFACT >= T;
+}
+
+// One entry from its 64 random bits (w0, w1), in two phases so that a quad's
+// table reads are issued together: qba_closed_rank (not-Q words, Lemire rank;
+// (p, h) identify the entry for the rare retry) then qba_closed_finish.
+struct QbaClosed {
+  uint32_t nq[4];
+  uint32_t rank, w0;
+};
+
+template <int NP>
+__device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
+                                                uint32_t k0, uint32_t k1, QbaClosed &c) {
+  using F = CF<NP>;
+  const uint32_t a = w1 & F::M4, b = (w1 >> 4) & F::M4, cc = (w0 >> 8) & F::M4, d = (w0 >> 12) & F::M4;
+  c.nq[0] = qba_perm_b(a, a, 0x02010000u);
+  c.nq[1] = qba_perm_b(b, a, 0x06050403u);
+  c.nq[2] = qba_perm_b(cc, b, 0x06050403u);
+  c.nq[3] = qba_perm_b(d, cc, 0x06050403u);
+  c.w0 = w0;
+  const bool o1 = qba_accept<NP>(w1, F::T32);
+  uint32_t rank = o1 ? w1 : (w0 & ~31u);
+  if (__builtin_expect(!o1 && !qba_accept<NP>(rank, F::T27), 0)) {  // ~(T32 T27) / 2^59 per entry
+    bool ok = false;
+    for (uint32_t t = 1; !ok; ++t) {
+      const QbaU4 y = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0x80000000u + t, h, k0, k1);
+      const uint32_t cand[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (!ok && qba_accept<NP>(cand[i], F::T32)) {
+          ok = true;
+          rank = cand[i];
+        }
+    }
+  }
+  c.rank = rank;
+}
+
+template <int NP>
+__device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint4 &A, const uint2 &sB,
+                                                  uint32_t sC, uint32_t (&D)[CF<NP>::ND]) {
+  using F = CF<NP>;
+  // A.w is zero in the table; folding it in keeps the read one ds_read_b128
+  // (4 LDS cycles) instead of a ds_read_b96 (8).
+  uint32_t q[4] = {A.x | A.w, A.y, A.z, A.w};
+  const uint32_t y0 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.x);
+  uint32_t y1 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.y);
+  if constexpr (F::RC > 1) y1 = qba_perm_b(y1, y0, sC);  // stage C moves window bytes 4..7 only
+  q[F::WIN] = y0;
+  q[F::WIN + 1] = y1;
+  const uint32_t R = ((c.w0 >> 1) & (uint32_t)(QCfg<NP>::W - 1)) * 0x01010101u;
+  const uint32_t qm = 0u - (c.w0 & 1u);  // all ones for a Q-correlated entry
+#pragma unroll
+  for (int i = 0; i < F::ND; ++i) D[i] = c.nq[i] ^ ((q[i] ^ R ^ c.nq[i]) & qm);
+}
+
+// Stage table indices of a rank and the LDS reads.
+template <int NP>
+__device__ __forceinline__ void qba_closed_tables(uint32_t rank, const uint32_t *__restrict__ pl,
+                                                  uint4 &A, uint2 &sB, uint32_t &sC) {
+  using F = CF<NP>;
+  uint32_t iA = 0, rem = rank;
+  if constexpr (F::RA > 1) {
+    const uint64_t pa = (uint64_t)rem * F::RA;
+    iA = (uint32_t)(pa >> 32);
+    rem = (uint32_t)pa;
+  }
+  const uint64_t pb = (uint64_t)rem * F::RB;
+  const uint32_t iB = (uint32_t)(pb >> 32);
+  const uint32_t iC = F::RC > 1 ? (uint32_t)(((uint64_t)(uint32_t)pb * F::RC) >> 32) : 0u;
+#ifdef QBA_EXP_NOTABLE
+  A = make_uint4(iA, iA * 3u, iA * 5u, 0u);
+  sB = make_uint2(iB, iB * 7u);
+  sC = iC * 9u;
+#else
+  A = *reinterpret_cast<const uint4 *>(pl + 4 * iA);
+  sB = *reinterpret_cast<const uint2 *>(pl + F::OFFB + 2 * iB);
+  sC = F::RC > 1 ? pl[F::OFFC + iC] : 0u;
+#endif
+}
+
+template <int NP>
+__device__ __forceinline__ void qba_closed_half(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
+                                                uint32_t k0, uint32_t k1,
+                                                const uint32_t *__restrict__ pl,
+                                                uint32_t (&D)[CF<NP>::ND]) {
+  QbaClosed c;
+  qba_closed_rank<NP>(w0, w1, p, h, k0, k1, c);
+  uint4 A;
+  uint2 sB;
+  uint32_t sC;
+  qba_closed_tables<NP>(c.rank, pl, A, sB, sC);
+  qba_closed_finish<NP>(c, A, sB, sC, D);
+}
+
+// Entry e on its own (odd pair alignment, tails): the half of its pair's block.
+template <int NP>
+__device__ __forceinline__ void qba_closed_entry(uint64_t e, uint32_t k0, uint32_t k1,
+                                                 const uint32_t *__restrict__ pl,
+                                                 uint32_t (&D)[CF<NP>::ND]) {
+  const uint64_t p = e >> 1;
+  const uint32_t h = (uint32_t)e & 1u;
+  const QbaU4 x = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0u, 0u, k0, k1);
+  qba_closed_half<NP>(h ? x.z : x.x, h ? x.w : x.y, p, h, k0, k1, pl, D);
+}
+
+// Outcome word of the table samplers -> byte layout.
+template <int NP>
+__device__ __forceinline__ void qba_out_to_d(typename QCfg<NP>::Out o, uint32_t (&D)[CF<NP>::ND]) {
+  using C = QCfg<NP>;
+#pragma unroll
+  for (int i = 0; i < CF<NP>::ND; ++i) D[i] = 0;
+#pragma unroll
+  for (int g = 0; g < C::G; ++g)
+    D[g / 4] |= ((uint32_t)(o >> C::shift(g)) & (uint32_t)C::M) << (8 * (g % 4));
+}
+
+// 4x4 byte transpose: r_i byte j = input j byte i (an involution).
+__device__ __forceinline__ void qba_t4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t &r0,
+                                       uint32_t &r1, uint32_t &r2, uint32_t &r3) {
+  const uint32_t t0 = qba_perm_b(b, a, 0x06020400u), t1 = qba_perm_b(b, a, 0x07030501u);
+  const uint32_t t2 = qba_perm_b(d, c, 0x06020400u), t3 = qba_perm_b(d, c, 0x07030501u);
+  r0 = qba_perm_b(t2, t0, 0x05040100u);
+  r1 = qba_perm_b(t3, t1, 0x05040100u);
+  r2 = qba_perm_b(t2, t0, 0x07060302u);
+  r3 = qba_perm_b(t3, t1, 0x07060302u);
+}
+
+// v_pk_lshlrev_b16: each 16-bit half of `one` shifted by the low 4 bits of
+// the same half of `amt` (the upper bits of the half are ignored by the ALU).
+__device__ __forceinline__ uint32_t qba_pk_onehot(uint32_t amt, uint32_t one) {
+  uint32_t r;
+  asm("v_pk_lshlrev_b16 %0, %1, %2" : "=v"(r) : "v"(amt), "v"(one));
+  return r;
+}
+
+typedef __attribute__((address_space(3))) uint32_t qba_lds_u32;  // LDS word (32-bit address)
+
+// base + byte b of x in one VALU op (v_add_u32 with an SDWA byte select)
+__device__ __forceinline__ uint32_t qba_add_byte(uint32_t base, uint32_t x, int b) {
+  uint32_t r;
+  switch (b) {
+    case 0: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(base), "v"(x)); break;
+    case 1: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(base), "v"(x)); break;
+    case 2: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(base), "v"(x)); break;
+    default: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(base), "v"(x)); break;
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// count one entry (group g = byte g % 4 of D[g / 4])
+//   Q-correlated iff L0 != L1 (tfg.py:327); u = L1 (tfg.py:182);
+//   H[u][g][L_g] += 1 for every g; C[u][g][h] += 1 for every equal pair --
+//   the pair loop runs only when the entry's distinct-value count (union of
+//   16-bit one-hots) is below n+1.
+// ---------------------------------------------------------------------------
+template <int NP>
+__device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uint32_t one,
+                                            uint32_t *hist) {
+  using C = QCfg<NP>;
+  using F = CF<NP>;
+  const uint32_t l0 = D[0] & 0xffu, l1 = (D[0] >> 8) & 0xffu;
+  if (l0 == l1) return;
+#ifdef QBA_EXP_NOCOUNT
+  if (l0 != 0xfffu) return;
+#endif
+  uint32_t bad = 0;
+#pragma unroll
+  for (int i = 0; i < F::ND; ++i) {
+    uint32_t vm = 0;  // bits that must be clear: value bits >= W of the real groups
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (4 * i + b < C::G) vm |= (0xffu & ~(uint32_t)(C::W - 1)) << (8 * b);
+    bad |= D[i] & vm;
+  }
+  if (bad) {
+    atomicAdd(&hist[C::HBL + C::CBL + 0], 1u);
+    return;
+  }
+  const uint32_t hb = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist + l1 * (uint32_t)(C::G * C::WP * 4);
+#pragma unroll
+  for (int i = 0; i < F::ND; ++i) {
+    const uint32_t E = D[i] << 2;  // byte b = 4 * value (< 64: no carry into the next byte)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int g = 4 * i + b;
+      if (g < C::G && g != 1) {  // H[u][1][x] = [x == u] |P_u|, derived when reduced
+        const uint32_t a = qba_add_byte(hb, E, b);
+        atomicAdd((uint32_t *)((qba_lds_u32 *)(uintptr_t)a + g * C::WP), 1u);
+      }
+    }
+  }
+#ifdef QBA_EXP_NOSEEN
+  return;
+#endif
+  uint32_t U = 0;
+#pragma unroll
+  for (int i = 0; i < F::ND; ++i) {
+    uint32_t mp = 0, mq = 0;
+    if (4 * i + 0 < C::G) mp |= 0x0000ffffu;
+    if (4 * i + 2 < C::G) mp |= 0xffff0000u;
+    if (4 * i + 1 < C::G) mq |= 0x0000ffffu;
+    if (4 * i + 3 < C::G) mq |= 0xffff0000u;
+    U |= (qba_pk_onehot(D[i], one) & mp) | (qba_pk_onehot(D[i] >> 8, one) & mq);
+  }
+  U = (U | (U >> 16)) & 0xffffu;
+  if (__popc(U) != C::G) {  // some pair collides: exact slow path
+    uint32_t l[C::G];
+#pragma unroll
+    for (int g = 0; g < C::G; ++g) l[g] = (D[g / 4] >> (8 * (g % 4))) & 0xffu;
+    uint32_t *c = hist + C::HBL + l1 * C::CP;
+    for (int g = 0; g < C::G; ++g)
+      for (int k = g + 1; k < C::G; ++k)
+        if (l[g] == l[k]) atomicAdd(&c[C::pidx(g, k)], 1u);
+  }
+}
+
+// Samplers of one entry into the byte layout
+enum { QBA_S_GENERAL = 0, QBA_S_FAST = 1, QBA_S_CLOSED = 2 };
+
+template <int NP, int SAMP>
+__device__ __forceinline__ void qba_entry_d(uint64_t e, uint32_t k0, uint32_t k1,
+                                            const QbaProgramSet *__restrict__ ps,
+                                            const uint64_t *pat, const uint64_t *apat,
+                                            const uint64_t *thr, const uint32_t *pl,
+                                            uint32_t (&D)[CF<NP>::ND]) {
+  if constexpr (SAMP == QBA_S_CLOSED) {
+    qba_closed_entry<NP>(e, k0, k1, pl, D);
+  } else if constexpr (SAMP == QBA_S_FAST) {
+    qba_out_to_d<NP>(qba_sample_entry_fast<NP>(e, k0, k1, ps->prog[1].perm_t, ps->prog[0].table_len, pat), D);
+  } else {
+    qba_out_to_d<NP>(qba_sample_entry<NP>(e, k0, k1, ps, pat, apat, thr), D);
+  }
+}
+
+// Sample one quad (entries [c0, c0+4) of the launch) into the byte layout.
+template <int NP, int SAMP, bool TAIL>
+__device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t first, uint32_t k0,
+                                                uint32_t k1, const QbaProgramSet *__restrict__ ps,
+                                                const uint64_t *pat, const uint64_t *apat,
+                                                const uint64_t *thr, const uint32_t *pl,
+                                                uint32_t (&D)[4][CF<NP>::ND]) {
+  constexpr int ND = CF<NP>::ND;
+  if constexpr (SAMP == QBA_S_CLOSED && !TAIL) {
+    if (!(first & 1)) {  // wave-uniform: the quad is two whole pairs
+      const uint64_t p0 = (first + c0) >> 1;
+      QbaClosed cl[4];
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const uint64_t p = p0 + jp;
+        const QbaU4 x = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0u, 0u, k0, k1);
+        qba_closed_rank<NP>(x.x, x.y, p, 0u, k0, k1, cl[2 * jp]);
+        qba_closed_rank<NP>(x.z, x.w, p, 1u, k0, k1, cl[2 * jp + 1]);
+      }
+      uint4 A[4];
+      uint2 sB[4];
+      uint32_t sC[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qba_closed_tables<NP>(cl[j].rank, pl, A[j], sB[j], sC[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qba_closed_finish<NP>(cl[j], A[j], sB[j], sC[j], D[j]);
+      return;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j < valid) {
+      qba_entry_d<NP, SAMP>(first + c0 + j, k0, k1, ps, pat, apat, thr, pl, D[j]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) D[j][i] = 0;
+    }
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void qba_count_quad(const uint32_t (&D)[4][CF<NP>::ND], int valid,
+                                               uint32_t *hist) {
+  const uint32_t one = 0x00010001u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < valid) qba_count_d<NP>(D[j], one, hist);
+}
+
+// One thread-step over QPT consecutive quads: entries [c0, c0 + 4 QPT) of the
+// launch (columns of `lists`).  Each list row is stored / loaded as one
+// 4*QPT-byte vector per thread (16 B at QPT = 4: a wave moves 1 KiB per row).
+// MODE 0: sample -> lists;  MODE 1: sample -> lists + counts;  MODE 2: lists -> counts
+// TAIL (QPT = 1 only): the last, partial quad, byte by byte.
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL>
+__device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
+                                         uint32_t k1, const QbaProgramSet *__restrict__ ps,
+                                         const uint64_t *pat, const uint64_t *apat,
+                                         const uint64_t *thr, const uint32_t *pl,
+                                         uint8_t *__restrict__ lists, uint64_t ld, uint32_t *hist) {
+  using C = QCfg<NP>;
+  constexpr int ND = CF<NP>::ND;
+  static_assert(QPT == 1 || QPT == 2 || QPT == 4, "QPT");
+  static_assert(!TAIL || QPT == 1, "tail quads are single");
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  using V = typename std::conditional<QPT == 4, u32x4, typename std::conditional<QPT == 2, u32x2, uint32_t>::type>::type;
+  const int valid = !TAIL ? 4 : ((count - c0) >= 4 ? 4 : (int)(count - c0));
+  uint32_t row[QPT][4 * ND];
+  uint32_t D[4][ND];
+  if constexpr (MODE == 2) {
+#pragma unroll
+    for (int k = 0; k < QPT; ++k)
+#pragma unroll
+      for (int g = 0; g < 4 * ND; ++g) row[k][g] = 0;
+    if (!TAIL) {
+#pragma unroll
+      for (int g = 0; g < C::G; ++g) {
+        const V v = __builtin_nontemporal_load(reinterpret_cast<const V *>(lists + (uint64_t)g * ld + c0));
+        const uint32_t *pv = reinterpret_cast<const uint32_t *>(&v);
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) row[k][g] = pv[k];
+      }
+    } else {
+      for (int g = 0; g < C::G; ++g)
+        for (int j = 0; j < valid; ++j) row[0][g] |= (uint32_t)lists[(uint64_t)g * ld + c0 + j] << (8 * j);
+    }
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+        qba_t4(row[k][4 * i], row[k][4 * i + 1], row[k][4 * i + 2], row[k][4 * i + 3], D[0][i],
+               D[1][i], D[2][i], D[3][i]);
+      qba_count_quad<NP>(D, valid, hist);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) {
+      qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+        qba_t4(D[0][i], D[1][i], D[2][i], D[3][i], row[k][4 * i], row[k][4 * i + 1],
+               row[k][4 * i + 2], row[k][4 * i + 3]);
+      if constexpr (MODE == 1) qba_count_quad<NP>(D, valid, hist);
+    }
+#ifdef QBA_EXP_NOSTORE
+    if (row[0][0] == 0x12345678u && row[0][1] == 0x9abcdef0u)
+#else
+    if (!TAIL)
+#endif
+    {
+#pragma unroll
+      for (int g = 0; g < C::G; ++g) {
+        V v;
+        uint32_t *pv = reinterpret_cast<uint32_t *>(&v);
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) pv[k] = row[k][g];
+        *reinterpret_cast<V *>(lists + (uint64_t)g * ld + c0) = v;
+      }
+    } else {
+      for (int g = 0; g < C::G; ++g)
+        for (int j = 0; j < valid; ++j) lists[(uint64_t)g * ld + c0 + j] = (uint8_t)(row[0][g] >> (8 * j));
+    }
+  }
+}
+
+// Stage the program's tables in LDS; returns the histogram base after them.
+template <int NP, int MODE, int SAMP, int BS>
+__device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__ ps, uint64_t *lds,
+                                               const uint64_t *&pat, const uint64_t *&apat,
+                                               const uint64_t *&thr, const uint32_t *&pl) {
+  pat = apat = thr = lds;
+  pl = reinterpret_cast<const uint32_t *>(lds);
+  uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
+  if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
+    for (int i = threadIdx.x; i < CF<NP>::WORDS; i += BS) dst[i] = src[i];
+    hist = dst + ((CF<NP>::WORDS + 3) & ~3);
+  } else if constexpr (MODE != 2) {
+    const int T = ps->table_total;
+    const uint64_t *tab = reinterpret_cast<const uint64_t *>(ps + 1);
+    const int ntab = ps->any_nonuniform ? 3 * T : T;
+    for (int i = threadIdx.x; i < ntab; i += BS) lds[i] = tab[i];
+    apat = lds + T;
+    thr = lds + 2 * T;
+    hist = reinterpret_cast<uint32_t *>(lds + ((ntab + 1) & ~1));  // 16-B aligned
+  }
+  return hist;
+}
+
+template <int NP, int MODE, int SAMP, int QPT>
+__global__ void __launch_bounds__(QBA_LBLOCK)
+    qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
+                uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
+                uint32_t *__restrict__ slab) {
+  using C = QCfg<NP>;
+  constexpr int BS = QBA_LBLOCK;
+  extern __shared__ __align__(16) uint64_t lds[];
+  const uint64_t *pat, *apat, *thr;
+  const uint32_t *pl;
+  uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
+  if (MODE != 0)
+    for (int i = threadIdx.x; i < C::NBP; i += BS) hist[i] = 0u;
+  __syncthreads();
+  const uint32_t nunits = count / (4 * QPT);
+  for (uint32_t u = blockIdx.x * BS + threadIdx.x; u < nunits; u += gridDim.x * BS)
+    qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
+                                         lists, ld, hist);
+  // the remaining < 4 QPT entries: whole quads, then the partial one
+  const uint32_t r0 = nunits * (4 * QPT), rq = (count - r0 + 3) >> 2;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x < rq) {
+    const uint32_t c0 = r0 + 4 * threadIdx.x;
+    if (c0 + 4 <= count)
+      qba_step<NP, MODE, SAMP, 1, false>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
+    else
+      qba_step<NP, MODE, SAMP, 1, true>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
+  }
+  if (MODE != 0) {
+    __syncthreads();
+    uint4 *dst = reinterpret_cast<uint4 *>(slab + (size_t)blockIdx.x * C::NBP);
+    const uint4 *src = reinterpret_cast<const uint4 *>(hist);
+    for (int i = threadIdx.x; i < C::NBP / 4; i += BS) dst[i] = src[i];
+  }
+}
+
+// Batched independent instances (BASELINE configs[3]): instance i is its own
+// run with Philox key seed_base + i over entries [0, count).  A workgroup
+// owns whole instances, so its LDS histogram IS the instance's final count
+// and is written out directly (no slab, no reduce launch).
+template <int NP, int SAMP>
+__global__ void __launch_bounds__(QBA_BLOCK)
+    qba_k_batched(const QbaProgramSet *__restrict__ ps, uint64_t seed_base, int64_t n_inst,
+                  uint64_t count, uint8_t *__restrict__ lists, uint64_t ld, uint64_t inst_stride,
+                  int64_t *__restrict__ H, int64_t *__restrict__ Cc, int64_t *__restrict__ P) {
+  using C = QCfg<NP>;
+  extern __shared__ __align__(16) uint64_t lds[];
+  const uint64_t *pat, *apat, *thr;
+  const uint32_t *pl;
+  uint32_t *hist = qba_stage<NP, 1, SAMP, QBA_BLOCK>(ps, lds, pat, apat, thr, pl);
+  for (int64_t inst = blockIdx.x; inst < n_inst; inst += gridDim.x) {
+    for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
+    __syncthreads();
+    const uint64_t key = seed_base + (uint64_t)inst;
+    uint8_t *L = lists + (uint64_t)inst * inst_stride;
+    const uint32_t nfull = (uint32_t)count >> 2;
+    for (uint32_t q = threadIdx.x; q < nfull; q += QBA_BLOCK)
+      qba_step<NP, 1, SAMP, 1, false>(q << 2, (uint32_t)count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps, pat,
+                                   apat, thr, pl, L, ld, hist);
+    if ((count & 3) && threadIdx.x == 0)
+      qba_step<NP, 1, SAMP, 1, true>(nfull << 2, (uint32_t)count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps,
+                                  pat, apat, thr, pl, L, ld, hist);
+    __syncthreads();
+    int64_t *h = H + inst * C::HB, *c = Cc + inst * C::CB, *p = P + inst * C::W;
+    for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = qba_hval<NP>(hist, i);
+    for (int r = threadIdx.x; r < C::CB; r += QBA_BLOCK) {
+      const int u = r / (C::G * C::G), g = (r / C::G) % C::G, k = r % C::G;
+      const int64_t v = g < k ? hist[C::HBL + u * C::CP + C::pidx(g, k)]
+                              : g > k ? hist[C::HBL + u * C::CP + C::pidx(k, g)]
+                                      : qba_psize<NP>(hist, u);
+      c[r] = v;
+    }
+    for (int u = threadIdx.x; u < C::W; u += QBA_BLOCK) p[u] = qba_psize<NP>(hist, u);
+    __syncthreads();
+  }
+}
+
+// Slab reduction.  Workgroup (x, y) sums slab rows [y*RP, (y+1)*RP) for 1024
+// bins (4 per thread, 16-B loads) and adds its partial into the u64
+// accumulator with integer atomics (order-independent: bitwise reproducible).
+#define QBA_RED_ROWS 32
+template <int NP>
+__global__ void __launch_bounds__(256)
+    qba_k_reduce(const uint32_t *__restrict__ slab, int nrows, unsigned long long *__restrict__ acc) {
+  using C = QCfg<NP>;
+  const int q = blockIdx.x * 256 + threadIdx.x;  // bin quad
+  if (4 * q >= C::NBP) return;
+  const int b0 = blockIdx.y * QBA_RED_ROWS;
+  const int b1 = b0 + QBA_RED_ROWS < nrows ? b0 + QBA_RED_ROWS : nrows;
+  unsigned long long s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll 8
+  for (int b = b0; b < b1; ++b) {
+    const uint4 v = reinterpret_cast<const uint4 *>(slab + (size_t)b * C::NBP)[q];
+    s0 += v.x;
+    s1 += v.y;
+    s2 += v.z;
+    s3 += v.w;
+  }
+  if (s0) atomicAdd(&acc[4 * q], s0);
+  if (s1) atomicAdd(&acc[4 * q + 1], s1);
+  if (s2) atomicAdd(&acc[4 * q + 2], s2);
+  if (s3) atomicAdd(&acc[4 * q + 3], s3);
+}
+
+// acc -> the int64 outputs (see qba.h for shapes): H as is (group 1's bins
+// derived, see qba_psize), C symmetrised with |P_u| on the diagonal, P, the
+// stats.  One workgroup: it stages the accumulator in LDS, zeroes it for the
+// next reduction (so no memset precedes one) and writes from the copy.
+template <int NP>
+__global__ void __launch_bounds__(1024)
+    qba_k_finalize(unsigned long long *__restrict__ acc, int64_t *__restrict__ H,
+                   int64_t *__restrict__ Cc, int64_t *__restrict__ P, int64_t *__restrict__ stats,
+                   int accumulate, int stats_accumulate) {
+  using C = QCfg<NP>;
+  __shared__ unsigned long long a[C::NBP];
+  for (int i = threadIdx.x; i < C::NBP; i += 1024) {
+    a[i] = acc[i];
+    acc[i] = 0ull;
+  }
+  __syncthreads();
+  auto put = [&](int64_t *dst, int64_t v) { *dst = accumulate ? *dst + v : v; };
+  for (int i = threadIdx.x; i < C::HB; i += 1024) put(&H[i], qba_hval<NP>(a, i));
+  for (int r = threadIdx.x; r < C::CB; r += 1024) {
+    const int u = r / (C::G * C::G), g = (r / C::G) % C::G, h = r % C::G;
+    if (g < h) {
+      const int64_t v = (int64_t)a[C::HBL + u * C::CP + C::pidx(g, h)];
+      put(&Cc[r], v);
+      put(&Cc[(u * C::G + h) * C::G + g], v);
+    } else if (g == h) {
+      put(&Cc[r], qba_psize<NP>(a, u));
+    }
+  }
+  if (threadIdx.x < C::W) put(&P[threadIdx.x], qba_psize<NP>(a, threadIdx.x));
+  if (threadIdx.x < C::STATS && stats)
+    stats[threadIdx.x] = (stats_accumulate ? stats[threadIdx.x] : 0) +
+                         (int64_t)a[C::HBL + C::CBL + threadIdx.x];
+}
+
+// ---------------------------------------------------------------------------
+// per-n launchers
+// ---------------------------------------------------------------------------
+
+// Persistent grid: every resident workgroup slot of the chip (LDS- and
+// register-limited occupancy), fewer when the launch has less work.
+static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, QBA_LBLOCK, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const uint64_t nquad = (count + 3) >> 2;
+  uint64_t g = (nquad + 4 * QBA_LBLOCK - 1) / (4 * QBA_LBLOCK);  // >= 4 quads per thread
+  const uint64_t cap = (uint64_t)ctx->num_cus * (uint64_t)per_cu;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// Sampler of the compiled pair: closed form when proven (n <= 11), else the
+// canonical-table fast path, else the general alias-table path.
+template <int NP>
+static int sampler_of(const QbaProgramSet *hs) {
+  if (NP <= QBA_CLOSED_MAX_N && hs->closed) return QBA_S_CLOSED;
+  return hs->canonical ? QBA_S_FAST : QBA_S_GENERAL;
+}
+
+// LDS bytes of the staged tables for a sampling launch
+template <int NP>
+static size_t table_lds(const QbaProgramSet *hs, int samp) {
+  if (samp == QBA_S_CLOSED) return (size_t)((CF<NP>::WORDS + 3) & ~3) * sizeof(uint32_t);
+  return (size_t)(((hs->any_nonuniform ? 3 : 1) * hs->table_total + 1) & ~1) * sizeof(uint64_t);
+}
+
+template <int NP>
+static int check_closed(const QbaProgramSet *hs) {
+  if (hs->closed && (hs->ra != CF<NP>::RA || hs->rb != CF<NP>::RB || hs->rc != CF<NP>::RC ||
+                     hs->perm_words != CF<NP>::WORDS || hs->t32 != CF<NP>::T32))
+    return qba_fail(QBA_EINVAL, "closed-form program does not match the kernel's stage layout");
+  return QBA_OK;
+}
+
+template <int NP>
+int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
+  using C = QCfg<NP>;
+  const QbaProgramSet *hs = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP]);
+  int samp = QBA_S_GENERAL;
+  size_t lds = 0;
+  if (L.mode != 2) {
+    samp = sampler_of<NP>(hs);
+    if (int rc = check_closed<NP>(hs)) return rc;
+    lds += table_lds<NP>(hs, samp);
+  }
+  if (L.mode != 0) lds += (size_t)C::NBP * sizeof(uint32_t);
+  lds = (lds + 15) & ~(size_t)15;
+  if (lds == 0) lds = 16;
+  // 4*QPT-byte row vectors (QPT quads per thread-step) when the rows allow it
+#ifdef QBA_EXP_NARROW
+  const bool wide = false;
+#else
+  constexpr uintptr_t VA = 4 * QBA_WIDE_QPT - 1;  // row vectors need their natural alignment
+  const bool wide = !(reinterpret_cast<uintptr_t>(L.lists) & VA) && !(L.ld & VA);
+#endif
+#define QBA_K(M, S) (wide ? (const void *)qba_k_lists<NP, M, S, QBA_WIDE_QPT> : (const void *)qba_k_lists<NP, M, S, 1>)
+  const void *kern = nullptr;
+  if (L.mode == 2) {
+    kern = QBA_K(2, QBA_S_GENERAL);
+  } else if (samp == QBA_S_CLOSED) {
+    if constexpr (NP <= QBA_CLOSED_MAX_N)
+      kern = L.mode == 0 ? QBA_K(0, QBA_S_CLOSED) : QBA_K(1, QBA_S_CLOSED);
+    else
+      return qba_fail(QBA_EUNSUPPORTED, "closed form beyond n = 11");
+  } else if (samp == QBA_S_FAST) {
+    kern = L.mode == 0 ? QBA_K(0, QBA_S_FAST) : QBA_K(1, QBA_S_FAST);
+  } else {
+    kern = L.mode == 0 ? QBA_K(0, QBA_S_GENERAL) : QBA_K(1, QBA_S_GENERAL);
+  }
+#undef QBA_K
+  if (lds > 65536) QBA_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int grid = grid_for(ctx, kern, lds, L.count);
+  uint32_t *slab = nullptr;
+  if (L.mode != 0) {
+    int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBP * sizeof(uint32_t));
+    if (rc) return rc;
+    slab = reinterpret_cast<uint32_t *>(ctx->slab);
+  }
+  const uint32_t k0 = (uint32_t)L.seed, k1 = (uint32_t)(L.seed >> 32);
+  const QbaProgramSet *ps = L.ps;
+  uint64_t first = L.first;
+  uint32_t count = (uint32_t)L.count;
+  uint8_t *lists = L.lists;
+  uint64_t ld = L.ld;
+  void *args[] = {&ps, (void *)&k0, (void *)&k1, &first, &count, &lists, &ld, &slab};
+  QBA_HIP(hipLaunchKernel(kern, dim3(grid), dim3(QBA_LBLOCK), args, lds, L.stream));
+  QBA_HIP(hipGetLastError());
+  int rc = QBA_OK;
+  if (rc || L.mode == 0) return rc;
+  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ctx->acc);
+  const dim3 rgrid((C::NBP / 4 + 255) / 256, (grid + QBA_RED_ROWS - 1) / QBA_RED_ROWS);
+  hipLaunchKernelGGL(qba_k_reduce<NP>, rgrid, dim3(256), 0, L.stream, slab, grid, acc);
+  QBA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(qba_k_finalize<NP>, dim3(1), dim3(1024), 0, L.stream, acc, L.H, L.C, L.P,
+                     L.stats, L.accumulate, L.stats_accumulate);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}
+
+template <int NP>
+int qba_launch_batched(qba_ctx *ctx, const QbaBatch &B) {
+  using C = QCfg<NP>;
+  const QbaProgramSet *hs = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP]);
+  const int samp = sampler_of<NP>(hs);
+  if (int rc = check_closed<NP>(hs)) return rc;
+  size_t lds = table_lds<NP>(hs, samp) + (size_t)C::NBINS * sizeof(uint32_t);
+  lds = (lds + 15) & ~(size_t)15;
+  const int64_t cap = (int64_t)ctx->num_cus * 16;
+  const int grid = (int)(B.n_inst < cap ? B.n_inst : cap);
+  auto go = [&](auto kern) -> int {
+    if (lds > 65536)
+      QBA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(QBA_BLOCK), lds, B.stream, B.ps, B.seed_base,
+                       B.n_inst, B.count, B.lists, B.ld, B.inst_stride, B.H, B.C, B.P);
+    QBA_HIP(hipGetLastError());
+    return QBA_OK;
+  };
+  if (samp == QBA_S_CLOSED) {
+    if constexpr (NP <= QBA_CLOSED_MAX_N) return go(qba_k_batched<NP, QBA_S_CLOSED>);
+    return qba_fail(QBA_EUNSUPPORTED, "closed form beyond n = 11");
+  }
+  return samp == QBA_S_FAST ? go(qba_k_batched<NP, QBA_S_FAST>) : go(qba_k_batched<NP, QBA_S_GENERAL>);
+}
+
