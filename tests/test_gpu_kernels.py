@@ -366,3 +366,62 @@ def test_chunked_launches(monkeypatch):
         assert np.array_equal(c2.numpy()[0], H)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("count", [1, 3, 4, 5, 7, 8, 9, 15, 17, 4099])
+def test_tiny_and_ragged_counts(engine, count):
+    """Tail handling: fewer entries than one thread-step, ragged remainders
+    (lists and counts vs the oracle, fused and check-only)."""
+    n, seed, first = 11, 2024, 10
+    info = engine.prepare(n)
+    lists, c = engine.sample_check(n, seed, first, count)
+    c2 = engine.check_counts(lists, n, count)
+    torch.cuda.synchronize()
+    got = lists[:, :count].cpu().numpy()
+    ref = oracle_lib.sample(n, seed, first, count, info["notq"], info["q"], info["closed"])
+    assert np.array_equal(got, ref)
+    H, C, P, bad = oracle_lib.counts(ref, n)
+    for cc in (c, c2):
+        gH, gC, gP = cc.numpy()
+        assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+
+
+def test_unaligned_rows_narrow_path(engine):
+    """Rows that are only 4-byte aligned (base offset 4, ld = 4 mod 8) run the
+    one-quad-per-step kernels; same lists and counts as the oracle."""
+    n, seed, count = 7, 77, 50_003
+    info = engine.prepare(n)
+    ld = (count + 63) // 64 * 64 + 4
+    buf = torch.zeros((n + 1, ld), dtype=torch.uint8, device=engine.device)
+    view = buf[:, 4:]
+    assert view.data_ptr() % 8 == 4 and view.stride(0) % 8 == 4
+    lists, c = engine.sample_check(n, seed, 1, count, lists=view)
+    c2 = engine.check_counts(view, n, count)
+    torch.cuda.synchronize()
+    got = view[:, :count].cpu().numpy()
+    ref = oracle_lib.sample(n, seed, 1, count, info["notq"], info["q"], info["closed"])
+    assert np.array_equal(got, ref)
+    assert not buf[:, :4].any() and not buf[:, 4 + count:].any()  # nothing written outside
+    H, C, P, bad = oracle_lib.counts(ref, n)
+    for cc in (c, c2):
+        gH, gC, gP = cc.numpy()
+        assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+
+
+def test_adversarial_collisions_wide_and_narrow(engine):
+    """Check-only mode on lists full of collisions (every Q entry has repeated
+    values): the pair slow path, on both row alignments, vs the oracle."""
+    n, count = 11, 30_001
+    rng = np.random.default_rng(5)
+    L = rng.integers(0, 4, (n + 1, count)).astype(np.uint8)  # 4 values for 12 groups
+    H, C, P, bad = oracle_lib.counts(L, n)
+    assert bad == 0 and C.sum() > P.sum() * (n + 1)
+    for off in (0, 4):
+        ld = (count + 63) // 64 * 64 + off
+        buf = torch.zeros((n + 1, ld), dtype=torch.uint8, device=engine.device)
+        view = buf[:, off:]
+        assert view.stride(0) % 8 == off
+        view[:, :count] = torch.from_numpy(L).to(engine.device)
+        c = engine.check_counts(view, n, count)
+        gH, gC, gP = c.numpy()
+        assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P), off
