@@ -9,8 +9,8 @@
 //     counts from registers.
 //
 // Layout: lists[g][k] uint8, row stride ld (SoA: a party's list is one row).
-// A thread owns 4 consecutive entries (one dword per row), so every row store
-// / load of a wave is 256 contiguous bytes.  Histograms are privatised per
+// A thread owns 2 x 4 consecutive entries per step (8 B per row), so every row
+// store / load of a wave is 512 contiguous bytes.  Histograms are privatised per
 // workgroup in LDS and flushed as u32 partials to a slab that a second
 // kernel reduces into int64 (bitwise reproducible, no global atomics).
 #pragma once
@@ -20,6 +20,9 @@
 
 #ifndef QBA_WIDE_QPT  // quads per thread-step of the wide kernels (experiment builds: 4)
 #define QBA_WIDE_QPT 2
+#endif
+#ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
+#define QBA_NT_STORE 1
 #endif
 
 
@@ -599,7 +602,14 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
         uint32_t *pv = reinterpret_cast<uint32_t *>(&v);
 #pragma unroll
         for (int k = 0; k < QPT; ++k) pv[k] = row[k][g];
-        *reinterpret_cast<V *>(lists + (uint64_t)g * ld + c0) = v;
+        V *dst = reinterpret_cast<V *>(lists + (uint64_t)g * ld + c0);
+#if QBA_NT_STORE
+        // the rows are streamed out once: nontemporal stores move the 12 rows of
+        // 1.25e8 entries in 0.313 ms instead of 0.356 (tools/ubench/stores2)
+        __builtin_nontemporal_store(v, dst);
+#else
+        *dst = v;
+#endif
       }
     } else {
       for (int g = 0; g < C::G; ++g)
@@ -648,7 +658,11 @@ __global__ void __launch_bounds__(QBA_LBLOCK)
     for (int i = threadIdx.x; i < C::NBP; i += BS) hist[i] = 0u;
   __syncthreads();
   const uint32_t nunits = count / (4 * QPT);
-  for (uint32_t u = blockIdx.x * BS + threadIdx.x; u < nunits; u += gridDim.x * BS)
+  // the grid stride in an SGPR, read once: reloading gridDim in the loop is a
+  // scalar load whose s_waitcnt lgkmcnt(0) also drains every LDS atomic the
+  // wave has in flight (-2% step time)
+  const uint32_t ustride = __builtin_amdgcn_readfirstlane(gridDim.x * BS);
+  for (uint32_t u = blockIdx.x * BS + threadIdx.x; u < nunits; u += ustride)
     qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
                                          lists, ld, hist);
   // the remaining < 4 QPT entries: whole quads, then the partial one
