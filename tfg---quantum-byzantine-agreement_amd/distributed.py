@@ -24,16 +24,22 @@ def shard_bounds(total: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 def world_from_env() -> Tuple[int, int, int]:
-    """(rank, local_rank, world_size) from torchrun's environment (1-process default)."""
-    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
-            int(os.environ.get("WORLD_SIZE", "1")))
+    """(rank, local_rank, world_size) from torchrun's environment (1-process default).
+
+    QBA_SHARE_DEVICE=1 maps every local rank to device 0: a rehearsal of the
+    N-rank path on a one-GPU box (with QBA_DIST_BACKEND=gloo, since RCCL
+    refuses two ranks on one device).  Never set for a measurement."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("QBA_SHARE_DEVICE") == "1":
+        local = 0
+    return int(os.environ.get("RANK", "0")), local, int(os.environ.get("WORLD_SIZE", "1"))
 
 
 def init(backend: Optional[str] = None) -> Tuple[int, int, int]:
     rank, local, world = world_from_env()
     if world > 1 and not torch.distributed.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("QBA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         torch.distributed.init_process_group(backend=backend)
