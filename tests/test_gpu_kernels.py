@@ -193,6 +193,34 @@ def test_counts_accumulate_and_invalid(engine):
     assert engine.last_stats()[0] == 3
 
 
+@pytest.mark.parametrize("n", [3, 11])
+def test_counts_out_of_range_values(engine, n):
+    """Values >= W (tfg.py:94 Cond2) in Q and in not-Q entries, scattered so
+    that some waves see one and others none: the quad-level range test must
+    fall back to the per-entry test exactly (stats[0] = bad Q entries, which
+    add nothing to H / C / P; not-Q entries are never counted)."""
+    count = 50_000
+    lists = engine.sample(n, 77, 0, count)
+    torch.cuda.synchronize()
+    L = lists[:, :count].cpu().numpy().copy()
+    rng = np.random.default_rng(n)
+    isq = np.nonzero(L[0] != L[1])[0]
+    notq = np.nonzero(L[0] == L[1])[0]
+    for k in rng.choice(isq, 7, replace=False):  # bad Q entries
+        L[rng.integers(2, n + 1), k] = rng.integers(1 << oracle_lib.n_qubits(n), 256)
+    for k in rng.choice(notq, 5, replace=False):  # bad not-Q entries: not counted at all
+        L[rng.integers(2, n + 1), k] = 255
+    k = isq[0]  # a bad Q entry that also collides
+    L[2, k], L[3, k] = 250, 250
+    d = torch.zeros_like(lists)
+    d[:, :count] = torch.from_numpy(L)
+    c = engine.check_counts(d, n, count)
+    gH, gC, gP = c.numpy()
+    H, C, P, bad = oracle_lib.counts(L, n)
+    assert bad == engine.last_stats()[0] >= 7
+    assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 5])
 def test_full_statevector_vs_oracle(engine, n):
     gates = json.loads((GOLDEN / "gates.json").read_text())[str(n)]

@@ -21,6 +21,9 @@
 #ifndef QBA_WIDE_QPT  // quads per thread-step of the wide kernels (experiment builds: 4)
 #define QBA_WIDE_QPT 2
 #endif
+#ifndef QBA_QUAD_RANGE  // count: one range test per quad of entries (experiment builds: 0)
+#define QBA_QUAD_RANGE 1
+#endif
 #ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
 #define QBA_NT_STORE 1
 #endif
@@ -399,6 +402,13 @@ __device__ __forceinline__ uint32_t qba_add_byte(uint32_t base, uint32_t x, int 
   return r;
 }
 
+// value of group g (runtime g) of an entry whose byte-layout words are w0..w3
+__device__ __forceinline__ uint32_t qba_byte_of(int g, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  const int i = g >> 2;
+  const uint32_t w = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+  return (w >> (8 * (g & 3))) & 0xffu;
+}
+
 // ---------------------------------------------------------------------------
 // count one entry (group g = byte g % 4 of D[g / 4])
 //   Q-correlated iff L0 != L1 (tfg.py:327); u = L1 (tfg.py:182);
@@ -408,7 +418,7 @@ __device__ __forceinline__ uint32_t qba_add_byte(uint32_t base, uint32_t x, int 
 // ---------------------------------------------------------------------------
 template <int NP>
 __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uint32_t one,
-                                            uint32_t *hist) {
+                                            uint32_t *hist, bool in_range) {
   using C = QCfg<NP>;
   using F = CF<NP>;
   const uint32_t l0 = D[0] & 0xffu, l1 = (D[0] >> 8) & 0xffu;
@@ -425,6 +435,7 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
       if (4 * i + b < C::G) vm |= (0xffu & ~(uint32_t)(C::W - 1)) << (8 * b);
     bad |= D[i] & vm;
   }
+  if (in_range) bad = 0;  // the caller's quad-level test found no value >= W
   if (bad) {
     atomicAdd(&hist[C::HBL + C::CBL + 0], 1u);
     return;
@@ -457,13 +468,19 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
   }
   U = (U | (U >> 16)) & 0xffffu;
   if (__popc(U) != C::G) {  // some pair collides: exact slow path
-    uint32_t l[C::G];
-#pragma unroll
-    for (int g = 0; g < C::G; ++g) l[g] = (D[g / 4] >> (8 * (g % 4))) & 0xffu;
+    // a compact loop (values picked by selects, no private array): this
+    // path is rare and unrolling it would multiply the kernel's code size
     uint32_t *c = hist + C::HBL + l1 * C::CP;
-    for (int g = 0; g < C::G; ++g)
-      for (int k = g + 1; k < C::G; ++k)
-        if (l[g] == l[k]) atomicAdd(&c[C::pidx(g, k)], 1u);
+    const uint32_t w0 = D[0], w1 = F::ND > 1 ? D[F::ND > 1 ? 1 : 0] : 0u,
+                   w2 = F::ND > 2 ? D[F::ND > 2 ? 2 : 0] : 0u, w3 = F::ND > 3 ? D[F::ND > 3 ? 3 : 0] : 0u;
+    int pi = 0;
+#pragma nounroll
+    for (int g = 0; g < C::G; ++g) {
+      const uint32_t lg = qba_byte_of(g, w0, w1, w2, w3);
+#pragma nounroll
+      for (int k = g + 1; k < C::G; ++k, ++pi)
+        if (lg == qba_byte_of(k, w0, w1, w2, w3)) atomicAdd(&c[pi], 1u);
+    }
   }
 }
 
@@ -525,13 +542,31 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
   }
 }
 
+// Every value of a quad of entries < W?  One OR over the quad's transposed
+// row words (about 2 VALU per entry) instead of a range test per entry; a
+// wave with any out-of-range value takes the per-entry test.
+template <int NP>
+__device__ __forceinline__ bool qba_rows_in_range(const uint32_t *row) {
+  using C = QCfg<NP>;
+  uint32_t o = 0;
+#pragma unroll
+  for (int g = 0; g < C::G; ++g) o |= row[g];
+  return !__any((o & (0xffu & ~(uint32_t)(C::W - 1)) * 0x01010101u) != 0u);  // wave-uniform
+}
+
 template <int NP>
 __device__ __forceinline__ void qba_count_quad(const uint32_t (&D)[4][CF<NP>::ND], int valid,
-                                               uint32_t *hist) {
+                                               uint32_t *hist, const uint32_t *row) {
   const uint32_t one = 0x00010001u;
+  if (QBA_QUAD_RANGE && qba_rows_in_range<NP>(row)) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (j < valid) qba_count_d<NP>(D[j], one, hist);
+    for (int j = 0; j < 4; ++j)
+      if (j < valid) qba_count_d<NP>(D[j], one, hist, true);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < valid) qba_count_d<NP>(D[j], one, hist, false);
+  }
 }
 
 // One thread-step over QPT consecutive quads: entries [c0, c0 + 4 QPT) of the
@@ -578,7 +613,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
       for (int i = 0; i < ND; ++i)
         qba_t4(row[k][4 * i], row[k][4 * i + 1], row[k][4 * i + 2], row[k][4 * i + 3], D[0][i],
                D[1][i], D[2][i], D[3][i]);
-      qba_count_quad<NP>(D, valid, hist);
+      qba_count_quad<NP>(D, valid, hist, row[k]);
     }
   } else {
 #pragma unroll
@@ -588,7 +623,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
       for (int i = 0; i < ND; ++i)
         qba_t4(D[0][i], D[1][i], D[2][i], D[3][i], row[k][4 * i], row[k][4 * i + 1],
                row[k][4 * i + 2], row[k][4 * i + 3]);
-      if constexpr (MODE == 1) qba_count_quad<NP>(D, valid, hist);
+      if constexpr (MODE == 1) qba_count_quad<NP>(D, valid, hist, row[k]);
     }
 #ifdef QBA_EXP_NOSTORE
     if (row[0][0] == 0x12345678u && row[0][1] == 0x9abcdef0u)
