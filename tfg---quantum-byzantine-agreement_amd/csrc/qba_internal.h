@@ -17,7 +17,7 @@
 #define QBA_MAX_TABLE 4096   // uint64 table entries per kind (LDS budget)
 #define QBA_BLOCK 256        // threads per workgroup (batched / helper kernels)
 #ifndef QBA_LBLOCK
-#define QBA_LBLOCK 512       // threads per workgroup of the streaming list kernels
+#define QBA_LBLOCK 768       // threads per workgroup of the streaming list kernels (2 per CU at n = 11)
 #endif
 #define QBA_CHUNK (1ull << 31)  // entries per list-kernel launch (32-bit offsets, u32 bins)
 #define QBA_EPT 4            // entries per thread per step: one dword per list row

@@ -21,6 +21,9 @@
 #ifndef QBA_WIDE_QPT  // quads per thread-step of the wide kernels (experiment builds: 4)
 #define QBA_WIDE_QPT 2
 #endif
+#ifndef QBA_QUEUE  // count Q entries 64 at a time from a per-wave LDS queue
+#define QBA_QUEUE 1
+#endif
 #ifndef QBA_QUAD_RANGE  // count: one range test per quad of entries (experiment builds: 0)
 #define QBA_QUAD_RANGE 1
 #endif
@@ -569,6 +572,52 @@ __device__ __forceinline__ void qba_count_quad(const uint32_t (&D)[4][CF<NP>::ND
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-level Q-entry queue (QBA_QUEUE): only Q entries are counted, so with
+// per-entry counting half the lanes of every count instruction idle.  Each
+// wave appends its Q entries (byte-layout words, SoA in LDS) to a ring of
+// QBA_QCAP slots and counts them 64 at a time with every lane busy.  All
+// queue state is wave-uniform and pushes / drains run with the full wave
+// (the callers keep exec full), so no entry is lost or counted twice.
+// ---------------------------------------------------------------------------
+#define QBA_QCAP 128
+template <int NP>
+__device__ __forceinline__ bool qba_isq_d(const uint32_t (&D)[CF<NP>::ND]) {
+  return ((D[0] ^ (D[0] >> 8)) & 0xffu) != 0u;  // L0 != L1 (tfg.py:327)
+}
+struct QbaWaveQ {
+  uint32_t *buf;  // [ND][QBA_QCAP] words of this wave
+  uint32_t tail, qn;
+};
+
+template <int NP>
+__device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_t nv) {
+  constexpr int ND = CF<NP>::ND;
+  const uint32_t lane = __lane_id();
+  const uint32_t slot = (q.tail + lane) & (QBA_QCAP - 1);
+  uint32_t D[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) D[i] = q.buf[i * QBA_QCAP + slot];
+  if (lane < nv) qba_count_d<NP>(D, 0x00010001u, hist, false);
+  q.tail = (q.tail + nv) & (QBA_QCAP - 1);
+  q.qn -= nv;
+}
+
+template <int NP>
+__device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], bool isq,
+                                           uint32_t *hist) {
+  constexpr int ND = CF<NP>::ND;
+  const uint64_t m = __ballot(isq);
+  const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (isq) {
+    const uint32_t slot = (q.tail + q.qn + pre) & (QBA_QCAP - 1);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) q.buf[i * QBA_QCAP + slot] = D[i];
+  }
+  q.qn += (uint32_t)__popcll(m);
+  if (q.qn >= 64) qba_q_drain<NP>(q, hist, 64);
+}
+
 // One thread-step over QPT consecutive quads: entries [c0, c0 + 4 QPT) of the
 // launch (columns of `lists`).  Each list row is stored / loaded as one
 // 4*QPT-byte vector per thread (16 B at QPT = 4: a wave moves 1 KiB per row).
@@ -579,7 +628,8 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
                                          uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                          const uint64_t *pat, const uint64_t *apat,
                                          const uint64_t *thr, const uint32_t *pl,
-                                         uint8_t *__restrict__ lists, uint64_t ld, uint32_t *hist) {
+                                         uint8_t *__restrict__ lists, uint64_t ld, uint32_t *hist,
+                                         QbaWaveQ *wq = nullptr, bool act = true) {
   using C = QCfg<NP>;
   constexpr int ND = CF<NP>::ND;
   static_assert(QPT == 1 || QPT == 2 || QPT == 4, "QPT");
@@ -595,7 +645,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
     for (int k = 0; k < QPT; ++k)
 #pragma unroll
       for (int g = 0; g < 4 * ND; ++g) row[k][g] = 0;
-    if (!TAIL) {
+    if (!TAIL && act) {
 #pragma unroll
       for (int g = 0; g < C::G; ++g) {
         const V v = __builtin_nontemporal_load(reinterpret_cast<const V *>(lists + (uint64_t)g * ld + c0));
@@ -603,7 +653,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
 #pragma unroll
         for (int k = 0; k < QPT; ++k) row[k][g] = pv[k];
       }
-    } else {
+    } else if (TAIL) {
       for (int g = 0; g < C::G; ++g)
         for (int j = 0; j < valid; ++j) row[0][g] |= (uint32_t)lists[(uint64_t)g * ld + c0 + j] << (8 * j);
     }
@@ -613,7 +663,12 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
       for (int i = 0; i < ND; ++i)
         qba_t4(row[k][4 * i], row[k][4 * i + 1], row[k][4 * i + 2], row[k][4 * i + 3], D[0][i],
                D[1][i], D[2][i], D[3][i]);
-      qba_count_quad<NP>(D, valid, hist, row[k]);
+      if (wq) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qba_q_push<NP>(*wq, D[j], act && qba_isq_d<NP>(D[j]), hist);
+      } else {
+        qba_count_quad<NP>(D, valid, hist, row[k]);
+      }
     }
   } else {
 #pragma unroll
@@ -623,12 +678,19 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
       for (int i = 0; i < ND; ++i)
         qba_t4(D[0][i], D[1][i], D[2][i], D[3][i], row[k][4 * i], row[k][4 * i + 1],
                row[k][4 * i + 2], row[k][4 * i + 3]);
-      if constexpr (MODE == 1) qba_count_quad<NP>(D, valid, hist, row[k]);
+      if constexpr (MODE == 1) {
+        if (wq) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) qba_q_push<NP>(*wq, D[j], act && qba_isq_d<NP>(D[j]), hist);
+        } else {
+          qba_count_quad<NP>(D, valid, hist, row[k]);
+        }
+      }
     }
 #ifdef QBA_EXP_NOSTORE
     if (row[0][0] == 0x12345678u && row[0][1] == 0x9abcdef0u)
 #else
-    if (!TAIL)
+    if (!TAIL && act)
 #endif
     {
 #pragma unroll
@@ -646,7 +708,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
         *dst = v;
 #endif
       }
-    } else {
+    } else if (TAIL) {
       for (int g = 0; g < C::G; ++g)
         for (int j = 0; j < valid; ++j) lists[(uint64_t)g * ld + c0 + j] = (uint8_t)(row[0][g] >> (8 * j));
     }
@@ -697,9 +759,24 @@ __global__ void __launch_bounds__(QBA_LBLOCK)
   // scalar load whose s_waitcnt lgkmcnt(0) also drains every LDS atomic the
   // wave has in flight (-2% step time)
   const uint32_t ustride = __builtin_amdgcn_readfirstlane(gridDim.x * BS);
-  for (uint32_t u = blockIdx.x * BS + threadIdx.x; u < nunits; u += ustride)
-    qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
-                                         lists, ld, hist);
+  if constexpr (MODE != 0 && QBA_QUEUE) {
+    QbaWaveQ wq;
+    wq.buf = hist + ((C::NBP + 3) & ~3) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP);
+    wq.tail = 0;
+    wq.qn = 0;
+    // wave-uniform trip count: pushes and drains always run with the whole wave
+    for (uint32_t u = blockIdx.x * BS + threadIdx.x;; u += ustride) {
+      const bool act = u < nunits;
+      if (!__any(act)) break;
+      qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
+                                           lists, ld, hist, &wq, act);
+    }
+    if (wq.qn) qba_q_drain<NP>(wq, hist, wq.qn);
+  } else {
+    for (uint32_t u = blockIdx.x * BS + threadIdx.x; u < nunits; u += ustride)
+      qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
+                                           lists, ld, hist);
+  }
   // the remaining < 4 QPT entries: whole quads, then the partial one
   const uint32_t r0 = nunits * (4 * QPT), rq = (count - r0 + 3) >> 2;
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x < rq) {
@@ -872,7 +949,10 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     if (int rc = check_closed<NP>(hs)) return rc;
     lds += table_lds<NP>(hs, samp);
   }
-  if (L.mode != 0) lds += (size_t)C::NBP * sizeof(uint32_t);
+  if (L.mode != 0) {
+    lds += (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
+    if (QBA_QUEUE) lds += (size_t)(QBA_LBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t);
+  }
   lds = (lds + 15) & ~(size_t)15;
   if (lds == 0) lds = 16;
   // 4*QPT-byte row vectors (QPT quads per thread-step) when the rows allow it
