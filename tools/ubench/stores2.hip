@@ -30,6 +30,22 @@ __global__ void __launch_bounds__(512) k_stride(unsigned char *L, size_t ld, uns
   }
 }
 
+// 8 B per lane of data, stored as 16 B by one lane of each lane pair (the
+// pair's partner row alternates with the row parity): 32 lanes x 16 B per row
+template <bool NT, int ROWS>
+__global__ void __launch_bounds__(512) k_pairx4(unsigned char *L, size_t ld, unsigned nvec8) {
+  for (unsigned q = blockIdx.x * 512 + threadIdx.x; q < nvec8; q += gridDim.x * 512) {
+    const unsigned par = threadIdx.x & 1;
+#pragma unroll
+    for (int g = 0; g < ROWS; ++g) {
+      if ((unsigned)(g & 1) == par) {
+        v4u v = mk<v4u>(q, g);
+        st<v4u, NT>(reinterpret_cast<v4u *>(L + g * ld + (size_t)(q & ~1u) * 8), v);
+      }
+    }
+  }
+}
+
 // workgroup b owns vectors [b*per, (b+1)*per) of every row
 template <typename T, bool NT, int ROWS>
 __global__ void __launch_bounds__(512) k_block(unsigned char *L, size_t ld, unsigned nvec) {
@@ -70,6 +86,16 @@ static void go(const char *name, unsigned char *L, size_t bytes_per_row, int gri
          (double)ROWS * bytes_per_row / (ms * 1e-3) / 1e12);
 }
 
+template <bool NT>
+static void go_pair(const char *name, unsigned char *L, size_t bytes_per_row, int grid) {
+  const unsigned nvec8 = (unsigned)(bytes_per_row / 8);
+  auto launch = [](unsigned char *L, size_t ld, unsigned nvec, int grid) {
+    hipLaunchKernelGGL((k_pairx4<NT, 12>), dim3(grid), dim3(512), 0, 0, L, ld, nvec);
+  };
+  const float ms = timeit(launch, L, bytes_per_row, nvec8, grid);
+  printf("%-28s grid %5d  %.3f ms  %.2f TB/s\n", name, grid, ms, 12.0 * bytes_per_row / (ms * 1e-3) / 1e12);
+}
+
 int main() {
   const size_t entries = 125000000ull / 64 * 64;
   unsigned char *L;
@@ -84,6 +110,8 @@ int main() {
     go<v4u, true, 12, true>("12row x4 block nt", L, entries, grid);
     go<v4u, false, 1, false>("1row x4 stride", L, 12 * entries, grid);
     go<v4u, true, 1, false>("1row x4 stride nt", L, 12 * entries, grid);
+    go_pair<true>("12row pair-x4 nt", L, entries, grid);
+    go_pair<false>("12row pair-x4", L, entries, grid);
   }
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
