@@ -236,6 +236,34 @@ def test_full_statevector_vs_oracle(engine, n):
         assert np.array_equal(idx, ridx) and np.max(np.abs(prob - rprob)) < 1e-12
 
 
+@pytest.mark.parametrize("q", [1, 2, 3, 5, 10])
+def test_statevector_random_circuits_fused_runs(engine, q):
+    """Random H / X / CX lists with long runs of X gates and of CX gates that
+    share a control (those runs become one XOR-mask pass each, incl. repeated
+    targets that cancel, bit 0 in the mask and the control on bit 0) -- vs the
+    dense oracle, which applies every gate on its own."""
+    rng = np.random.default_rng(1000 + q)
+    for trial in range(6):
+        ops = []
+        while len(ops) < 40:
+            kind = rng.integers(3)
+            if kind == 0:
+                ops.append(("H", int(rng.integers(q)), -1))
+            elif kind == 1:
+                for _ in range(int(rng.integers(1, 6))):
+                    ops.append(("X", int(rng.integers(q)), -1))
+            elif q > 1:
+                c = int(rng.integers(q))
+                for _ in range(int(rng.integers(1, 8))):
+                    t = int(rng.integers(q - 1))
+                    ops.append(("X", t + (t >= c), c))
+        trip = np.array([(0 if g == "H" else 1, t, c) for g, t, c in ops], np.int32)
+        sv = engine.statevector(q, trip)
+        torch.cuda.synchronize()
+        ref = sv_oracle.run(ops, q)
+        assert np.max(np.abs(sv.cpu().numpy() - ref)) < 1e-12, (q, trial)
+
+
 def test_ghz_register_statevector(engine):
     """One entangled register of the Q resource (n+1 qubits) at n=19: support
     {0...0, 1...1}, each 1/2 (the per-register closed form of A2)."""

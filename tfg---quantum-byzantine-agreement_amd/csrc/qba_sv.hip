@@ -3,9 +3,11 @@
 // q qubits is 2^q doubles (8 B each; 2^35 = 275 GB is the largest that fits
 // one MI355X).  Qubit 0 is the most significant bit of the basis index.
 //
-// Every gate is one streaming pass over the state: each thread moves 16 B
-// (a double2) per access whenever the touched bits allow it, so a pass is
-// bound by HBM at 16 B of traffic per amplitude (8 B read + 8 B written).
+// Every H gate is one streaming pass over the state, and every RUN of X
+// gates or of CX gates sharing a control is one XOR-mask pass (gate fusion,
+// qba_k_sv_xmask); each thread moves 16 B (a double2) per access whenever
+// the touched bits allow it, so a pass is bound by HBM at 16 B of traffic
+// per amplitude it moves (8 B read + 8 B written).
 #include "qba_compact.h"
 
 static constexpr double kInvSqrt2 = 0.70710678118654752440;
@@ -21,50 +23,62 @@ __global__ void qba_k_sv_init(double2 *__restrict__ sv, uint64_t n2) {
     sv[i] = make_double2(i == 0 ? 1.0 : 0.0, 0.0);
 }
 
-// kind: 0 = H, 1 = X.  b = bit position of the target (nq-1-target).
+// Hadamard on the qubit at bit position b (nq-1-target).
 // b >= 1: thread t handles the two adjacent pairs rooted at ins0(2t, b).
-template <int KIND>
-__global__ void qba_k_sv_1q(double *__restrict__ sv, int b, uint64_t nthreads) {
+__global__ void qba_k_sv_h(double *__restrict__ sv, int b, uint64_t nthreads) {
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nthreads;
        t += (uint64_t)gridDim.x * blockDim.x) {
     if (b == 0) {
       double2 *p = reinterpret_cast<double2 *>(sv) + t;
       const double2 a = *p;
-      *p = KIND == 0 ? make_double2((a.x + a.y) * kInvSqrt2, (a.x - a.y) * kInvSqrt2)
-                     : make_double2(a.y, a.x);
+      *p = make_double2((a.x + a.y) * kInvSqrt2, (a.x - a.y) * kInvSqrt2);
     } else {
       const uint64_t i0 = qba_ins0(2 * t, b);
       double2 *p0 = reinterpret_cast<double2 *>(sv + i0);
       double2 *p1 = reinterpret_cast<double2 *>(sv + i0 + (1ull << b));
       const double2 a = *p0, c = *p1;
-      if (KIND == 0) {
-        *p0 = make_double2((a.x + c.x) * kInvSqrt2, (a.y + c.y) * kInvSqrt2);
-        *p1 = make_double2((a.x - c.x) * kInvSqrt2, (a.y - c.y) * kInvSqrt2);
-      } else {
-        *p0 = c;
-        *p1 = a;
-      }
+      *p0 = make_double2((a.x + c.x) * kInvSqrt2, (a.y + c.y) * kInvSqrt2);
+      *p1 = make_double2((a.x - c.x) * kInvSqrt2, (a.y - c.y) * kInvSqrt2);
     }
   }
 }
 
-// controlled X: bc = control bit position, bt = target bit position.
-// Threads enumerate indices with both bits clear; when neither bit is 0 a
-// thread handles two adjacent indices with double2 accesses.
-__global__ void qba_k_sv_cx(double *__restrict__ sv, int bc, int bt, uint64_t nthreads, int vec) {
-  const int blo = bc < bt ? bc : bt, bhi = bc < bt ? bt : bc;
+// XOR-mask permutation, optionally controlled: every index i with the
+// control bit set (bc < 0: every index) swaps amplitudes with i ^ M.  One
+// controlled X is M = 1 << bt; a run of CX gates sharing a control (they
+// commute: all targets differ from the control) or a run of X gates is the
+// XOR of their target bits, so a whole run costs one pass (the Q resource's
+// GHZ register: n CX gates from qubit 0 -> one pass, tfg.py:38-39).
+// Threads enumerate the pair representatives (bit brep = the HIGHEST bit of
+// M clear, control bit set), two adjacent indices (i, i+1) per thread with
+// double2 accesses when neither brep nor the control is bit 0.  The partner
+// of that pair is (i^M, (i+1)^M): the aligned double2 at i^M when bit 0 is
+// not in M, else the one at (i+1)^M = (i^M) - 1 with its halves swapped.
+// Consecutive threads therefore touch contiguous bytes on both sides even
+// when M holds low bits (they only mirror the order inside a block).
+__global__ void qba_k_sv_xmask(double *__restrict__ sv, int bc, int brep, uint64_t M, uint64_t nthreads,
+                               int vec) {
+  const int blo = (bc >= 0 && bc < brep) ? bc : brep, bhi = (bc >= 0 && bc < brep) ? brep : bc;
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nthreads;
        t += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t i = vec ? 2 * t : t;
+    i = qba_ins0(i, blo);
+    if (bc >= 0) i = qba_ins0(i, bhi) | (1ull << bc);
+    const uint64_t j = i ^ M;
     if (vec) {
-      const uint64_t i = qba_ins0(qba_ins0(2 * t, blo), bhi) | (1ull << bc);
       double2 *p0 = reinterpret_cast<double2 *>(sv + i);
-      double2 *p1 = reinterpret_cast<double2 *>(sv + (i | (1ull << bt)));
       const double2 a = *p0;
-      *p0 = *p1;
-      *p1 = a;
+      if (M & 1ull) {
+        double2 *p1 = reinterpret_cast<double2 *>(sv + (j - 1));
+        const double2 c = *p1;
+        *p0 = make_double2(c.y, c.x);
+        *p1 = make_double2(a.y, a.x);
+      } else {
+        double2 *p1 = reinterpret_cast<double2 *>(sv + j);
+        *p0 = *p1;
+        *p1 = a;
+      }
     } else {
-      const uint64_t i = qba_ins0(qba_ins0(t, blo), bhi) | (1ull << bc);
-      const uint64_t j = i | (1ull << bt);
       const double a = sv[i];
       sv[i] = sv[j];
       sv[j] = a;
@@ -101,27 +115,43 @@ extern "C" int qba_sv_apply(qba_ctx *ctx, double *sv, int nq, const int32_t *gat
   int rc = qba_set_device(ctx);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
+  // runs of X gates (ctl -1) or of CX gates sharing a control fold into one
+  // XOR-mask pass; H gates are one butterfly pass each
+  int run_ctl = -2;  // -2: no open run
+  uint64_t run_mask = 0;
+  auto flush = [&]() -> int {
+    if (run_ctl != -2 && run_mask) {
+      const int bc = run_ctl < 0 ? -1 : nq - 1 - run_ctl;
+      const int brep = 63 - __builtin_clzll(run_mask);
+      const int vec = (brep != 0 && bc != 0 && nq >= (bc >= 0 ? 3 : 2)) ? 1 : 0;
+      const uint64_t npairs = (1ull << (nq - 1)) >> (bc >= 0 ? 1 : 0);
+      const uint64_t nthr = npairs / (vec ? 2 : 1);
+      hipLaunchKernelGGL(qba_k_sv_xmask, dim3(sv_grid(nthr)), dim3(256), 0, s, sv, bc, brep, run_mask, nthr,
+                         vec);
+      QBA_HIP(hipGetLastError());
+    }
+    run_ctl = -2;
+    run_mask = 0;
+    return QBA_OK;
+  };
   for (int g = 0; g < ngates; ++g) {
     const int32_t k = gates[3 * g], t = gates[3 * g + 1], c = gates[3 * g + 2];
     const int bt = nq - 1 - t;
-    if (c < 0) {
-      const uint64_t nthr = bt == 0 ? (1ull << (nq - 1)) : (1ull << (nq - 1)) / 2;
-      if (nq == 1 && bt == 0) {
-        // a single pair handled by one thread
+    if (k == QBA_GATE_X) {
+      const int ctl = c < 0 ? -1 : c;
+      if (ctl != run_ctl) {
+        if (int e = flush()) return e;
+        run_ctl = ctl;
       }
-      if (k == QBA_GATE_H)
-        hipLaunchKernelGGL(qba_k_sv_1q<0>, dim3(sv_grid(nthr)), dim3(256), 0, s, sv, bt, nthr);
-      else
-        hipLaunchKernelGGL(qba_k_sv_1q<1>, dim3(sv_grid(nthr)), dim3(256), 0, s, sv, bt, nthr);
-    } else {
-      const int bc = nq - 1 - c;
-      const int vec = (bt >= 1 && bc >= 1 && nq >= 3) ? 1 : 0;
-      const uint64_t nthr = (1ull << (nq - 2)) / (vec ? 2 : 1);
-      hipLaunchKernelGGL(qba_k_sv_cx, dim3(sv_grid(nthr)), dim3(256), 0, s, sv, bc, bt, nthr, vec);
+      run_mask ^= 1ull << bt;
+      continue;
     }
+    if (int e = flush()) return e;
+    const uint64_t nthr = bt == 0 ? (1ull << (nq - 1)) : (1ull << (nq - 1)) / 2;
+    hipLaunchKernelGGL(qba_k_sv_h, dim3(sv_grid(nthr)), dim3(256), 0, s, sv, bt, nthr);
     QBA_HIP(hipGetLastError());
   }
-  return QBA_OK;
+  return flush();
 }
 
 struct QbaSupportPred {
