@@ -48,10 +48,7 @@ extern "C" int qba_init(int device, qba_ctx **out) {
     if (v >= 4 && v <= QBA_CHUNK) ctx->chunk = v;
   }
   if (hipMalloc(&ctx->flag, 64) != hipSuccess || hipMalloc(&ctx->count1, 64) != hipSuccess ||
-      hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess ||
-      hipMalloc(&ctx->acc, (16 * 16 * 17 + 16 * 16 * 16 + 16) * 8) != hipSuccess ||
-      hipMemset(ctx->acc, 0, (16 * 16 * 17 + 16 * 16 * 16 + 16) * 8) != hipSuccess ||
-      hipMalloc(&ctx->ticket, 64) != hipSuccess || hipMemset(ctx->ticket, 0, 64) != hipSuccess) {
+      hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess) {
     delete ctx;
     return qba_fail(QBA_ENOMEM, "qba_init: hipMalloc of flags failed");
   }
@@ -71,8 +68,6 @@ extern "C" int qba_destroy(qba_ctx *ctx) {
   if (ctx->flag) (void)hipFree(ctx->flag);
   if (ctx->count1) (void)hipFree(ctx->count1);
   if (ctx->stats) (void)hipFree(ctx->stats);
-  if (ctx->acc) (void)hipFree(ctx->acc);
-  if (ctx->ticket) (void)hipFree(ctx->ticket);
   delete ctx;
   return QBA_OK;
 }

@@ -156,8 +156,6 @@ struct qba_ctx {
   int32_t *flag = nullptr;  // 1-word device flag
   int64_t *count1 = nullptr; // 1-word device counter
   int64_t *stats = nullptr;  // [2]: last counts launch: Q entries with a value >= w, spare
-  void *acc = nullptr;       // u64 column sums of the slab (max bins of any n); kept zeroed
-  unsigned int *ticket = nullptr;  // arrival counter of the reduce launch; kept zeroed
   uint64_t chunk = QBA_CHUNK;  // entries per list-kernel launch (env QBA_CHUNK_ENTRIES, tests)
 };
 

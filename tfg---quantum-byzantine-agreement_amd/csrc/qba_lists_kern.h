@@ -740,19 +740,43 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   return hist;
 }
 
+#ifndef QBA_ZERO_AT_END
+#define QBA_ZERO_AT_END 1
+#endif
+// The outputs of a counting launch start at zero unless the call accumulates:
+// the list kernel's workgroup 0 clears them before the reduction adds in.
+struct QbaZero {
+  int64_t *H, *C, *P, *stats;
+  uint32_t flags;  // bit 0: clear H, C, P; bit 1: clear the stats
+};
+template <int NP>
+__device__ __forceinline__ void qba_zero_outputs(const QbaZero &z, int tid, int bs) {
+  using C = QCfg<NP>;
+  if (z.flags & 1) {
+    for (int i = tid; i < C::HB; i += bs) z.H[i] = 0;
+    for (int i = tid; i < C::CB; i += bs) z.C[i] = 0;
+    for (int i = tid; i < C::W; i += bs) z.P[i] = 0;
+  }
+  if ((z.flags & 2) && z.stats && tid < C::STATS) z.stats[tid] = 0;
+}
+
 template <int NP, int MODE, int SAMP, int QPT>
 __global__ void __launch_bounds__(QBA_LBLOCK)
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                 uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
-                uint32_t *__restrict__ slab) {
+                uint32_t *__restrict__ slab, QbaZero zero) {
   using C = QCfg<NP>;
   constexpr int BS = QBA_LBLOCK;
   extern __shared__ __align__(16) uint64_t lds[];
   const uint64_t *pat, *apat, *thr;
   const uint32_t *pl;
   uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
-  if (MODE != 0)
+  if (MODE != 0) {
     for (int i = threadIdx.x; i < C::NBP; i += BS) hist[i] = 0u;
+#if !QBA_ZERO_AT_END
+    if (blockIdx.x == 0) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
+#endif
+  }
   __syncthreads();
   const uint32_t nunits = count / (4 * QPT);
   // the grid stride in an SGPR, read once: reloading gridDim in the loop is a
@@ -791,6 +815,11 @@ __global__ void __launch_bounds__(QBA_LBLOCK)
     uint4 *dst = reinterpret_cast<uint4 *>(slab + (size_t)blockIdx.x * C::NBP);
     const uint4 *src = reinterpret_cast<const uint4 *>(hist);
     for (int i = threadIdx.x; i < C::NBP / 4; i += BS) dst[i] = src[i];
+#if QBA_ZERO_AT_END
+    // any point of this kernel precedes the reduction; at the end it leaves
+    // the main loop's code placement alone
+    if (blockIdx.x == gridDim.x - 1) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
+#endif
   }
 }
 
@@ -835,65 +864,70 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   }
 }
 
-// Slab reduction.  Workgroup (x, y) sums slab rows [y*RP, (y+1)*RP) for 1024
-// bins (4 per thread, 16-B loads) and adds its partial into the u64
-// accumulator with integer atomics (order-independent: bitwise reproducible).
+// Slab reduction straight into the int64 outputs (see qba.h for shapes).
+// Workgroup (x, y) sums slab rows [y*RP, (y+1)*RP) for 1024 bins (4 per
+// thread, 16-B loads) and adds each nonzero partial to the output word(s) the
+// bin maps to with integer atomics (order-independent: bitwise
+// reproducible): H as counted; a pair bin to C[u][g][h] and C[u][h][g]; group
+// 0's bins also to |P_u| -- summed per workgroup in LDS first -- which is P[u],
+// every C[u][g][g] and H[u][1][u] (group 1's bins are derived, see
+// qba_psize); the stats bins to the stats.  The list kernel of the same
+// launch zeroed the outputs unless the call accumulates, so no finalize pass
+// or accumulator is needed.
+#ifndef QBA_RED_ROWS  // slab rows per reduce workgroup
 #define QBA_RED_ROWS 32
+#endif
 template <int NP>
 __global__ void __launch_bounds__(256)
-    qba_k_reduce(const uint32_t *__restrict__ slab, int nrows, unsigned long long *__restrict__ acc) {
+    qba_k_reduce(const uint32_t *__restrict__ slab, int nrows, int64_t *__restrict__ H,
+                 int64_t *__restrict__ Cc, int64_t *__restrict__ P, int64_t *__restrict__ stats) {
   using C = QCfg<NP>;
-  const int q = blockIdx.x * 256 + threadIdx.x;  // bin quad
-  if (4 * q >= C::NBP) return;
-  const int b0 = blockIdx.y * QBA_RED_ROWS;
-  const int b1 = b0 + QBA_RED_ROWS < nrows ? b0 + QBA_RED_ROWS : nrows;
-  unsigned long long s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-#pragma unroll 8
-  for (int b = b0; b < b1; ++b) {
-    const uint4 v = reinterpret_cast<const uint4 *>(slab + (size_t)b * C::NBP)[q];
-    s0 += v.x;
-    s1 += v.y;
-    s2 += v.z;
-    s3 += v.w;
-  }
-  if (s0) atomicAdd(&acc[4 * q], s0);
-  if (s1) atomicAdd(&acc[4 * q + 1], s1);
-  if (s2) atomicAdd(&acc[4 * q + 2], s2);
-  if (s3) atomicAdd(&acc[4 * q + 3], s3);
-}
-
-// acc -> the int64 outputs (see qba.h for shapes): H as is (group 1's bins
-// derived, see qba_psize), C symmetrised with |P_u| on the diagonal, P, the
-// stats.  One workgroup: it stages the accumulator in LDS, zeroes it for the
-// next reduction (so no memset precedes one) and writes from the copy.
-template <int NP>
-__global__ void __launch_bounds__(1024)
-    qba_k_finalize(unsigned long long *__restrict__ acc, int64_t *__restrict__ H,
-                   int64_t *__restrict__ Cc, int64_t *__restrict__ P, int64_t *__restrict__ stats,
-                   int accumulate, int stats_accumulate) {
-  using C = QCfg<NP>;
-  __shared__ unsigned long long a[C::NBP];
-  for (int i = threadIdx.x; i < C::NBP; i += 1024) {
-    a[i] = acc[i];
-    acc[i] = 0ull;
-  }
+  typedef unsigned long long u64;
+  __shared__ u64 psz[C::W];
+  if (threadIdx.x < C::W) psz[threadIdx.x] = 0ull;
   __syncthreads();
-  auto put = [&](int64_t *dst, int64_t v) { *dst = accumulate ? *dst + v : v; };
-  for (int i = threadIdx.x; i < C::HB; i += 1024) put(&H[i], qba_hval<NP>(a, i));
-  for (int r = threadIdx.x; r < C::CB; r += 1024) {
-    const int u = r / (C::G * C::G), g = (r / C::G) % C::G, h = r % C::G;
-    if (g < h) {
-      const int64_t v = (int64_t)a[C::HBL + u * C::CP + C::pidx(g, h)];
-      put(&Cc[r], v);
-      put(&Cc[(u * C::G + h) * C::G + g], v);
-    } else if (g == h) {
-      put(&Cc[r], qba_psize<NP>(a, u));
+  const int q = blockIdx.x * 256 + threadIdx.x;  // bin quad
+  if (4 * q < C::NBP) {
+    const int b0 = blockIdx.y * QBA_RED_ROWS;
+    const int b1 = b0 + QBA_RED_ROWS < nrows ? b0 + QBA_RED_ROWS : nrows;
+    u64 s[4] = {0ull, 0ull, 0ull, 0ull};
+#pragma unroll 8
+    for (int b = b0; b < b1; ++b) {
+      const uint4 v = reinterpret_cast<const uint4 *>(slab + (size_t)b * C::NBP)[q];
+      s[0] += v.x;
+      s[1] += v.y;
+      s[2] += v.z;
+      s[3] += v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!s[j]) continue;
+      const int b = 4 * q + j;
+      if (b < C::HBL) {
+        const int u = b / (C::G * C::WP), r = b - u * C::G * C::WP, g = r / C::WP, x = r - g * C::WP;
+        if (x >= C::W || g == 1) continue;  // row padding / never counted
+        atomicAdd(reinterpret_cast<u64 *>(&H[(u * C::G + g) * C::W + x]), s[j]);
+        if (g == 0) atomicAdd(&psz[u], s[j]);
+      } else if (b < C::HBL + C::CBL) {
+        const int u = (b - C::HBL) / C::CP;
+        int p = b - C::HBL - u * C::CP, g = 0;
+        while (p >= C::G - 1 - g) p -= C::G - 1 - g++;  // pidx(g, h) inverted
+        const int h = g + 1 + p;
+        atomicAdd(reinterpret_cast<u64 *>(&Cc[(u * C::G + g) * C::G + h]), s[j]);
+        atomicAdd(reinterpret_cast<u64 *>(&Cc[(u * C::G + h) * C::G + g]), s[j]);
+      } else if (b < C::NBINS && stats) {
+        atomicAdd(reinterpret_cast<u64 *>(&stats[b - C::HBL - C::CBL]), s[j]);
+      }
     }
   }
-  if (threadIdx.x < C::W) put(&P[threadIdx.x], qba_psize<NP>(a, threadIdx.x));
-  if (threadIdx.x < C::STATS && stats)
-    stats[threadIdx.x] = (stats_accumulate ? stats[threadIdx.x] : 0) +
-                         (int64_t)a[C::HBL + C::CBL + threadIdx.x];
+  __syncthreads();
+  for (int i = threadIdx.x; i < C::W * (C::G + 2); i += 256) {
+    const int u = i / (C::G + 2), k = i - u * (C::G + 2);
+    const u64 v = psz[u];
+    if (!v) continue;
+    int64_t *dst = k < C::G ? &Cc[(u * C::G + k) * C::G + k] : k == C::G ? &P[u] : &H[(u * C::G + 1) * C::W + u];
+    atomicAdd(reinterpret_cast<u64 *>(dst), v);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -902,13 +936,18 @@ __global__ void __launch_bounds__(1024)
 
 // Persistent grid: every resident workgroup slot of the chip (LDS- and
 // register-limited occupancy), fewer when the launch has less work.
+#ifndef QBA_GRID_QPT
+#define QBA_GRID_QPT 2
+#endif
 static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, QBA_LBLOCK, lds) != hipSuccess ||
       per_cu < 1)
     per_cu = 1;
   const uint64_t nquad = (count + 3) >> 2;
-  uint64_t g = (nquad + 4 * QBA_LBLOCK - 1) / (4 * QBA_LBLOCK);  // >= 4 quads per thread
+  // >= 2 quads (one wide thread-step) per thread: a small launch (configs[1],
+  // 1e6 entries) spreads over 163 workgroups instead of 82
+  uint64_t g = (nquad + QBA_GRID_QPT * QBA_LBLOCK - 1) / (QBA_GRID_QPT * QBA_LBLOCK);
   const uint64_t cap = (uint64_t)ctx->num_cus * (uint64_t)per_cu;
   if (g > cap) g = cap;
   if (g < 1) g = 1;
@@ -991,17 +1030,14 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   uint32_t count = (uint32_t)L.count;
   uint8_t *lists = L.lists;
   uint64_t ld = L.ld;
-  void *args[] = {&ps, (void *)&k0, (void *)&k1, &first, &count, &lists, &ld, &slab};
+  QbaZero zero{L.H, L.C, L.P, L.stats,
+               (L.mode != 0 && !L.accumulate ? 1u : 0u) | (L.mode != 0 && !L.stats_accumulate ? 2u : 0u)};
+  void *args[] = {&ps, (void *)&k0, (void *)&k1, &first, &count, &lists, &ld, &slab, &zero};
   QBA_HIP(hipLaunchKernel(kern, dim3(grid), dim3(QBA_LBLOCK), args, lds, L.stream));
   QBA_HIP(hipGetLastError());
-  int rc = QBA_OK;
-  if (rc || L.mode == 0) return rc;
-  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ctx->acc);
+  if (L.mode == 0) return QBA_OK;
   const dim3 rgrid((C::NBP / 4 + 255) / 256, (grid + QBA_RED_ROWS - 1) / QBA_RED_ROWS);
-  hipLaunchKernelGGL(qba_k_reduce<NP>, rgrid, dim3(256), 0, L.stream, slab, grid, acc);
-  QBA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(qba_k_finalize<NP>, dim3(1), dim3(1024), 0, L.stream, acc, L.H, L.C, L.P,
-                     L.stats, L.accumulate, L.stats_accumulate);
+  hipLaunchKernelGGL(qba_k_reduce<NP>, rgrid, dim3(256), 0, L.stream, slab, grid, L.H, L.C, L.P, L.stats);
   QBA_HIP(hipGetLastError());
   return QBA_OK;
 }
