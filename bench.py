@@ -350,6 +350,9 @@ def config4(args, eng):
     # the fused CX pass reads and writes the control = 1 half once: 8 B per amplitude of the state
     gbs = 8 * (1 << q) / t / 1e9
     ok = len(idx) == 2 and abs(prob[0] - 0.5) < 1e-12 and abs(prob[1] - 0.5) < 1e-12
+    del sv
+    torch.cuda.empty_cache()
+    full = full_circuit_n7(eng)
     return _line(args, gbs, "GB/s (gate passes)",
                  f"BASELINE configs[4]: GHZ register of the Q resource, {q} qubits fp64 "
                  f"(n={q - 1} parties), {(8 << q) / 2 ** 30:.0f} GiB",
@@ -361,7 +364,47 @@ def config4(args, eng):
                  {"ms_per_step": t * 1e3,
                   "register_prep_ms": prep * 1e3, "cx_gates_fused_per_pass": q - 1,
                   "verification": {"support": [int(i) for i in idx], "probs": [float(p) for p in prob],
-                                   "ghz_exact": bool(ok)}}, dtype="f64")
+                                   "ghz_exact": bool(ok)},
+                  "full_circuit_n7": full}, dtype="f64")
+
+
+def full_circuit_n7(eng, n=7):
+    """configs[4]'s other reading: the largest n whose WHOLE
+    resource circuit fits as one dense state -- n = 7, 24 qubits, 128 MiB
+    real fp64.  Both of tfg.py's circuits (tfg.py:15-22, 25-40; pi fixed)
+    are prepared gate by gate on the device and their support is checked
+    exactly against the closed form: not-Q = W^n equiprobable words with
+    L0 = L1, Q = the W words {r ^ pi(g)} at 1/W each (qubit 0 = MSB)."""
+    import numpy as np
+    import torch
+    res = importlib.import_module(f"{PKG}.resource")
+    nq = res.n_qubits(n)
+    N, W = (n + 1) * nq, 1 << nq
+    perm = np.roll(np.arange(1, n + 1), 3)
+    out = {"qubits": N, "n_parties": n, "state_MiB": (8 << N) >> 20}
+    sv = torch.empty(1 << N, dtype=torch.float64, device=eng.device)
+    for kind, gate in (("notq", res.notQCorrelated(n, nq)), ("q", res.qCorrelated(n, nq, perm=perm))):
+        tri = gate.triples()
+        eng.statevector(N, tri, out=sv)  # warm
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        eng.statevector(N, tri, out=sv)
+        b.record()
+        torch.cuda.synchronize()
+        idx, prob = eng.support(sv, N, cap=1 << 22)
+        shift = [N - (g + 1) * nq for g in range(n + 1)]
+        if kind == "notq":
+            fields = np.stack([(idx >> s) & (W - 1) for s in shift])
+            exact = (len(idx) == W ** n and bool((fields[0] == fields[1]).all())
+                     and bool(np.all(np.abs(prob - float(W) ** -n) < 1e-12)))
+        else:
+            pi = np.concatenate([[0], perm])
+            want = np.sort([sum(int(r ^ pi[g]) << shift[g] for g in range(n + 1)) for r in range(W)])
+            exact = np.array_equal(np.sort(idx), want) and bool(np.all(np.abs(prob - 1.0 / W) < 1e-12))
+        out[kind] = {"gates": int(len(tri)), "prep_ms": a.elapsed_time(b), "support": int(len(idx)),
+                     "exact": bool(exact)}
+    return out
 
 
 def main():

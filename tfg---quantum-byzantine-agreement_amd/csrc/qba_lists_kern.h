@@ -421,11 +421,11 @@ __device__ __forceinline__ uint32_t qba_byte_of(int g, uint32_t w0, uint32_t w1,
 // ---------------------------------------------------------------------------
 template <int NP>
 __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uint32_t one,
-                                            uint32_t *hist, bool in_range) {
+                                            uint32_t *hist, bool in_range, bool known_q = false) {
   using C = QCfg<NP>;
   using F = CF<NP>;
   const uint32_t l0 = D[0] & 0xffu, l1 = (D[0] >> 8) & 0xffu;
-  if (l0 == l1) return;
+  if (!known_q && l0 == l1) return;  // the Q-entry queue holds only entries with L0 != L1
 #ifdef QBA_EXP_NOCOUNT
   if (l0 != 0xfffu) return;
 #endif
@@ -598,7 +598,7 @@ __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_
   uint32_t D[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) D[i] = q.buf[i * QBA_QCAP + slot];
-  if (lane < nv) qba_count_d<NP>(D, 0x00010001u, hist, false);
+  if (lane < nv) qba_count_d<NP>(D, 0x00010001u, hist, false, true);
   q.tail = (q.tail + nv) & (QBA_QCAP - 1);
   q.qn -= nv;
 }
