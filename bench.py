@@ -57,8 +57,10 @@ DATA = "synthetic: lists Born-sampled on the device (Philox4x32-10 keyed by entr
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: 200 for the headline, 20 otherwise)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps (default: 50 for the headline, 3 otherwise)")
     ap.add_argument("--config", type=int, default=2, choices=[0, 1, 2, 3, 4])
     ap.add_argument("--n", type=int, default=11)
     ap.add_argument("--dishonest", type=int, default=3)
@@ -409,6 +411,14 @@ def full_circuit_n7(eng, n=7):
 
 def main():
     args = parse()
+    # The headline's first ~40 launches after the GPU idles run 400-520 us and
+    # then settle at ~366 us for as long as the launches continue (per-launch
+    # kernel trace over 2050 launches: profiles/r1/launch_drift.txt), so its
+    # default window is 50 untimed + 200 timed launches (~0.1 s in total).
+    if args.steps is None:
+        args.steps = 200 if args.config == 2 else 20
+    if args.warmup is None:
+        args.warmup = 50 if args.config == 2 else 3
     if args.config == 2:
         headline(args)
         return
