@@ -193,6 +193,10 @@ def headline(args):
             "kernel": f"qba_k_lists<{n},1,*> + qba_k_reduce" if args.mode == "fused"
                       else f"qba_k_lists<{n},0,*> + qba_k_lists<{n},2,*> + reduce",
             "algorithmic_bytes_per_entry": bytes_per_entry, "launch_ms": kern_ms,
+            # the bytes the launch really moves (PMC) over the same time: the fused
+            # kernel never re-reads the lists, so this sits near half of frac
+            "traffic_gbs": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
+            "traffic_frac": traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
         },
         "verification": {"q_entries": int(Pn.sum()), "offdiag_collisions": offdiag},
     }
