@@ -580,7 +580,10 @@ __device__ __forceinline__ void qba_count_quad(const uint32_t (&D)[4][CF<NP>::ND
 // queue state is wave-uniform and pushes / drains run with the full wave
 // (the callers keep exec full), so no entry is lost or counted twice.
 // ---------------------------------------------------------------------------
-#define QBA_QCAP 128
+#ifndef QBA_QBATCH  // 64-entry batches counted per drain (one LDS wait per drain)
+#define QBA_QBATCH 1
+#endif
+#define QBA_QCAP (128 * QBA_QBATCH)
 template <int NP>
 __device__ __forceinline__ bool qba_isq_d(const uint32_t (&D)[CF<NP>::ND]) {
   return ((D[0] ^ (D[0] >> 8)) & 0xffu) != 0u;  // L0 != L1 (tfg.py:327)
@@ -603,6 +606,25 @@ __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_
   q.qn -= nv;
 }
 
+// QBA_QBATCH full batches: every batch's words are read before the first is
+// counted, so the drain waits on LDS once instead of once per batch
+template <int NP>
+__device__ __forceinline__ void qba_q_drain_full(QbaWaveQ &q, uint32_t *hist) {
+  constexpr int ND = CF<NP>::ND;
+  const uint32_t lane = __lane_id();
+  uint32_t D[QBA_QBATCH][ND];
+#pragma unroll
+  for (int j = 0; j < QBA_QBATCH; ++j) {
+    const uint32_t slot = (q.tail + 64 * j + lane) & (QBA_QCAP - 1);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) D[j][i] = q.buf[i * QBA_QCAP + slot];
+  }
+#pragma unroll
+  for (int j = 0; j < QBA_QBATCH; ++j) qba_count_d<NP>(D[j], 0x00010001u, hist, false, true);
+  q.tail = (q.tail + 64 * QBA_QBATCH) & (QBA_QCAP - 1);
+  q.qn -= 64 * QBA_QBATCH;
+}
+
 template <int NP>
 __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], bool isq,
                                            uint32_t *hist) {
@@ -615,7 +637,7 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
     for (int i = 0; i < ND; ++i) q.buf[i * QBA_QCAP + slot] = D[i];
   }
   q.qn += (uint32_t)__popcll(m);
-  if (q.qn >= 64) qba_q_drain<NP>(q, hist, 64);
+  if (q.qn >= 64 * QBA_QBATCH) qba_q_drain_full<NP>(q, hist);
 }
 
 // One thread-step over QPT consecutive quads: entries [c0, c0 + 4 QPT) of the
@@ -795,7 +817,7 @@ __global__ void __launch_bounds__(QBA_LBLOCK)
       qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
                                            lists, ld, hist, &wq, act);
     }
-    if (wq.qn) qba_q_drain<NP>(wq, hist, wq.qn);
+    while (wq.qn) qba_q_drain<NP>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
   } else {
     for (uint32_t u = blockIdx.x * BS + threadIdx.x; u < nunits; u += ustride)
       qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
