@@ -185,7 +185,10 @@ def headline(args):
                         f"{per:.3g} entries/GPU (sizeL={per * world:.3g} over {world} GPU)",
             "n_parties": n, "n_dishonest": args.dishonest, "entries_per_gpu": per,
             "sizeL": per * world, "mode": args.mode, "sampler": "closed" if info["closed"] else "tables",
-            "parallelism": f"sizeL sharded over {world} GPU(s), RCCL all-reduce of counts",
+            "parallelism": f"sizeL sharded over {world} GPU(s)" + (
+                ", one all-reduce of counts per step ("
+                + ("RCCL" if torch.distributed.get_backend() == "nccl" else torch.distributed.get_backend())
+                + ")" if world > 1 else ", no collective at N=1"),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
