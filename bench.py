@@ -65,7 +65,8 @@ def parse():
     ap.add_argument("--n", type=int, default=11)
     ap.add_argument("--dishonest", type=int, default=3)
     ap.add_argument("--per-gpu", type=float, default=1.25e8, help="entries per GPU per step")
-    ap.add_argument("--mode", choices=["fused", "split"], default="fused")
+    ap.add_argument("--mode", choices=["fused", "split", "sample"], default="fused",
+                    help="fused (the headline), split (sample then check), sample (diagnostic: no check)")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -122,6 +123,8 @@ def headline(args):
     def launch():
         if args.mode == "fused":
             eng.sample_check(n, args.seed, first, per, lists, counts)
+        elif args.mode == "sample":
+            eng.sample(n, args.seed, first, per, lists)
         else:
             eng.sample(n, args.seed, first, per, lists)
             eng.check_counts(lists, n, per, counts)

@@ -316,15 +316,21 @@ template <int NP>
 __device__ __forceinline__ void qba_closed_tables(uint32_t rank, const uint32_t *__restrict__ pl,
                                                   uint4 &A, uint2 &sB, uint32_t &sC) {
   using F = CF<NP>;
+  // Each digit is the high word of one v_mad_u64_u32; the empty asm makes
+  // it opaque so its table offset is ONE v_lshl_add (without it the compiler
+  // rebuilt digit * stride from the 64-bit product: alignbit + and + shift).
   uint32_t iA = 0, rem = rank;
   if constexpr (F::RA > 1) {
     const uint64_t pa = (uint64_t)rem * F::RA;
     iA = (uint32_t)(pa >> 32);
     rem = (uint32_t)pa;
+    asm("" : "+v"(iA));
   }
   const uint64_t pb = (uint64_t)rem * F::RB;
-  const uint32_t iB = (uint32_t)(pb >> 32);
-  const uint32_t iC = F::RC > 1 ? (uint32_t)(((uint64_t)(uint32_t)pb * F::RC) >> 32) : 0u;
+  uint32_t iB = (uint32_t)(pb >> 32);
+  asm("" : "+v"(iB));
+  uint32_t iC = F::RC > 1 ? (uint32_t)(((uint64_t)(uint32_t)pb * F::RC) >> 32) : 0u;
+  if constexpr (F::RC > 1) asm("" : "+v"(iC));
 #ifdef QBA_EXP_NOTABLE
   A = make_uint4(iA, iA * 3u, iA * 5u, 0u);
   sB = make_uint2(iB, iB * 7u);
@@ -580,64 +586,68 @@ __device__ __forceinline__ void qba_count_quad(const uint32_t (&D)[4][CF<NP>::ND
 // queue state is wave-uniform and pushes / drains run with the full wave
 // (the callers keep exec full), so no entry is lost or counted twice.
 // ---------------------------------------------------------------------------
-#ifndef QBA_QBATCH  // 64-entry batches counted per drain (one LDS wait per drain)
-#define QBA_QBATCH 1
-#endif
-#define QBA_QCAP (128 * QBA_QBATCH)
+#define QBA_QCAP 128  // ring slots per wave (two drains' worth)
+// L0 != L1 (tfg.py:327) for an active lane: am = 0xff on active lanes, 0 on
+// the idle lanes of the last step (one v_bitop3 + compare straight into VCC)
 template <int NP>
-__device__ __forceinline__ bool qba_isq_d(const uint32_t (&D)[CF<NP>::ND]) {
-  return ((D[0] ^ (D[0] >> 8)) & 0xffu) != 0u;  // L0 != L1 (tfg.py:327)
+__device__ __forceinline__ bool qba_isq_d(const uint32_t (&D)[CF<NP>::ND], uint32_t am = 0xffu) {
+  return ((D[0] ^ (D[0] >> 8)) & am) != 0u;
 }
 struct QbaWaveQ {
-  uint32_t *buf;  // [ND][QBA_QCAP] words of this wave
-  uint32_t tail, qn;
+  uint32_t base;      // LDS byte address of this wave's ring [ND][QBA_QCAP] words (aligned to 4 QBA_QCAP B)
+  uint32_t tail, qn;  // wave-uniform: first queued slot (not reduced mod QBA_QCAP), queued entries
 };
 
+// LDS byte address of ring slot s (any integer: taken mod QBA_QCAP); the
+// ring's alignment makes the slot bits an OR into the base
+__device__ __forceinline__ uint32_t qba_q_addr(const QbaWaveQ &q, uint32_t s) {
+  return ((s & (QBA_QCAP - 1)) << 2) | q.base;
+}
+__device__ __forceinline__ qba_lds_u32 *qba_lds(uint32_t addr) {
+  return reinterpret_cast<qba_lds_u32 *>(static_cast<uintptr_t>(addr));
+}
+
+// The queue area starts after the histogram, aligned to one ring (the host
+// sizes the launch's LDS with QBA_QCAP * 4 bytes of slack for it).
 template <int NP>
+__device__ __forceinline__ uint32_t qba_queue_base(uint32_t *hist) {
+  const uint32_t h = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist + ((QCfg<NP>::NBP + 3) & ~3) * 4;
+  return (h + QBA_QCAP * 4 - 1) & ~(uint32_t)(QBA_QCAP * 4 - 1);
+}
+
+// Count the nv (<= 64) oldest queued entries, one per lane.  TRUSTED: the
+// values were produced by this kernel's sampler, masked to nq bits, so
+// Cond2's range test cannot fail and is skipped (check-only launches keep it).
+template <int NP, bool TRUSTED>
 __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_t nv) {
   constexpr int ND = CF<NP>::ND;
   const uint32_t lane = __lane_id();
-  const uint32_t slot = (q.tail + lane) & (QBA_QCAP - 1);
+  const uint32_t a = qba_q_addr(q, q.tail + lane);
   uint32_t D[ND];
 #pragma unroll
-  for (int i = 0; i < ND; ++i) D[i] = q.buf[i * QBA_QCAP + slot];
-  if (lane < nv) qba_count_d<NP>(D, 0x00010001u, hist, false, true);
-  q.tail = (q.tail + nv) & (QBA_QCAP - 1);
+  for (int i = 0; i < ND; ++i) D[i] = *qba_lds(a + i * QBA_QCAP * 4);
+  if (nv >= 64 || lane < nv) qba_count_d<NP>(D, 0x00010001u, hist, TRUSTED, true);
+  q.tail += nv;
   q.qn -= nv;
 }
 
-// QBA_QBATCH full batches: every batch's words are read before the first is
-// counted, so the drain waits on LDS once instead of once per batch
-template <int NP>
-__device__ __forceinline__ void qba_q_drain_full(QbaWaveQ &q, uint32_t *hist) {
-  constexpr int ND = CF<NP>::ND;
-  const uint32_t lane = __lane_id();
-  uint32_t D[QBA_QBATCH][ND];
-#pragma unroll
-  for (int j = 0; j < QBA_QBATCH; ++j) {
-    const uint32_t slot = (q.tail + 64 * j + lane) & (QBA_QCAP - 1);
-#pragma unroll
-    for (int i = 0; i < ND; ++i) D[j][i] = q.buf[i * QBA_QCAP + slot];
-  }
-#pragma unroll
-  for (int j = 0; j < QBA_QBATCH; ++j) qba_count_d<NP>(D[j], 0x00010001u, hist, false, true);
-  q.tail = (q.tail + 64 * QBA_QBATCH) & (QBA_QCAP - 1);
-  q.qn -= 64 * QBA_QBATCH;
-}
-
-template <int NP>
+// Append the lanes' entries with isq set (in lane order) and count a full
+// batch of 64 as soon as one is queued.  Slot = tail + qn + the number of
+// queued lanes below this one (mbcnt adds the base for free).
+template <int NP, bool TRUSTED>
 __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], bool isq,
                                            uint32_t *hist) {
   constexpr int ND = CF<NP>::ND;
   const uint64_t m = __ballot(isq);
-  const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  const uint32_t slot =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, q.tail + q.qn));
   if (isq) {
-    const uint32_t slot = (q.tail + q.qn + pre) & (QBA_QCAP - 1);
+    const uint32_t a = qba_q_addr(q, slot);
 #pragma unroll
-    for (int i = 0; i < ND; ++i) q.buf[i * QBA_QCAP + slot] = D[i];
+    for (int i = 0; i < ND; ++i) *qba_lds(a + i * QBA_QCAP * 4) = D[i];
   }
   q.qn += (uint32_t)__popcll(m);
-  if (q.qn >= 64 * QBA_QBATCH) qba_q_drain_full<NP>(q, hist);
+  if (q.qn >= 64) qba_q_drain<NP, TRUSTED>(q, hist, 64u);
 }
 
 // One thread-step over QPT consecutive quads: entries [c0, c0 + 4 QPT) of the
@@ -662,6 +672,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
   const int valid = !TAIL ? 4 : ((count - c0) >= 4 ? 4 : (int)(count - c0));
   uint32_t row[QPT][4 * ND];
   uint32_t D[4][ND];
+  const uint32_t am = act ? 0xffu : 0u;
   if constexpr (MODE == 2) {
 #pragma unroll
     for (int k = 0; k < QPT; ++k)
@@ -687,7 +698,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
                D[1][i], D[2][i], D[3][i]);
       if (wq) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) qba_q_push<NP>(*wq, D[j], act && qba_isq_d<NP>(D[j]), hist);
+        for (int j = 0; j < 4; ++j) qba_q_push<NP, MODE == 1>(*wq, D[j], qba_isq_d<NP>(D[j], am), hist);
       } else {
         qba_count_quad<NP>(D, valid, hist, row[k]);
       }
@@ -703,7 +714,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
       if constexpr (MODE == 1) {
         if (wq) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) qba_q_push<NP>(*wq, D[j], act && qba_isq_d<NP>(D[j]), hist);
+          for (int j = 0; j < 4; ++j) qba_q_push<NP, MODE == 1>(*wq, D[j], qba_isq_d<NP>(D[j], am), hist);
         } else {
           qba_count_quad<NP>(D, valid, hist, row[k]);
         }
@@ -807,7 +818,7 @@ __global__ void __launch_bounds__(QBA_LBLOCK)
   const uint32_t ustride = __builtin_amdgcn_readfirstlane(gridDim.x * BS);
   if constexpr (MODE != 0 && QBA_QUEUE) {
     QbaWaveQ wq;
-    wq.buf = hist + ((C::NBP + 3) & ~3) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP);
+    wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
     wq.qn = 0;
     // wave-uniform trip count: pushes and drains always run with the whole wave
@@ -817,7 +828,7 @@ __global__ void __launch_bounds__(QBA_LBLOCK)
       qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
                                            lists, ld, hist, &wq, act);
     }
-    while (wq.qn) qba_q_drain<NP>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
+    while (wq.qn) qba_q_drain<NP, MODE == 1>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
   } else {
     for (uint32_t u = blockIdx.x * BS + threadIdx.x; u < nunits; u += ustride)
       qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
@@ -1012,7 +1023,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   }
   if (L.mode != 0) {
     lds += (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
-    if (QBA_QUEUE) lds += (size_t)(QBA_LBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t);
+    if (QBA_QUEUE) lds += (size_t)(QBA_LBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
   }
   lds = (lds + 15) & ~(size_t)15;
   if (lds == 0) lds = 16;
