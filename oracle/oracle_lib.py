@@ -87,5 +87,36 @@ def sample_counts(n: int, seed: int, first: int, count: int, prog_notq: dict, pr
     return lists[:, :count], H, Cc, P
 
 
+def _counts_buffers(n: int, lead=()):
+    w = 1 << n_qubits(n)
+    return (np.zeros(lead + (w, n + 1, w), np.int64), np.zeros(lead + (w, n + 1, n + 1), np.int64),
+            np.zeros(lead + (w,), np.int64))
+
+
+def stream_counts(n: int, seed: int, first: int, count: int, prog_notq: dict, prog_q: dict,
+                  closed: bool = False):
+    """H, C, P, bad over entries [first, first+count) sampled and counted
+    without storing the lists (any size)."""
+    H, Cc, P = _counts_buffers(n)
+    k0, a0 = _prog_args(prog_notq)
+    k1, a1 = _prog_args(prog_q)
+    lib().oracle_stream_counts.restype = C.c_int64
+    bad = lib().oracle_stream_counts(C.c_int(n), C.c_uint64(seed), C.c_uint64(first), C.c_uint64(count),
+                                     C.c_int(int(closed)), *a0, *a1, _p(H), _p(Cc), _p(P))
+    return H, Cc, P, int(bad)
+
+
+def batched_counts(n: int, seed_base: int, n_inst: int, count: int, prog_notq: dict, prog_q: dict,
+                   closed: bool = False):
+    """Per-instance H, C, P of n_inst independent runs (key seed_base + i,
+    entries [0, count)), as [n_inst, ...] arrays."""
+    H, Cc, P = _counts_buffers(n, (n_inst,))
+    k0, a0 = _prog_args(prog_notq)
+    k1, a1 = _prog_args(prog_q)
+    lib().oracle_batched_counts(C.c_int(n), C.c_uint64(seed_base), C.c_int64(n_inst), C.c_uint64(count),
+                                C.c_int(int(closed)), *a0, *a1, _p(H), _p(Cc), _p(P))
+    return H, Cc, P
+
+
 def threads() -> int:
     return int(lib().oracle_threads())

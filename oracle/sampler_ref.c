@@ -319,6 +319,96 @@ int64_t oracle_sample_counts(int n, uint64_t seed, uint64_t first, uint64_t coun
   return oracle_counts(n, lists, count, ld, H, Cc, P);
 }
 
+/* values of one entry (either schedule) into vals[0..n] */
+static void entry_values(int n, uint64_t seed, uint64_t e, int closed, const prog_t *p0, const prog_t *p1,
+                         uint64_t t, uint8_t vals[16]) {
+  if (closed) {
+    closed_entry(n, seed, e, vals);
+    return;
+  }
+  const uint64_t out = sample_outcome(n, seed, e, p0, p1, t);
+  const int nq = n_qubits(n), N = (n + 1) * nq;
+  for (int g = 0; g <= n; ++g) vals[g] = (uint8_t)((out >> (N - (g + 1) * nq)) & ((1u << nq) - 1u));
+}
+
+/* count one entry from its values (same rules as count_column) */
+static void count_values(const uint8_t *l, int n, int w, int64_t *H, int64_t *Cc, int64_t *bad) {
+  const int G = n + 1;
+  if (l[0] == l[1]) return;
+  for (int g = 0; g < G; ++g)
+    if (l[g] >= w) {
+      ++*bad;
+      return;
+    }
+  const int u = l[1];
+  for (int g = 0; g < G; ++g) H[((int64_t)u * G + g) * w + l[g]] += 1;
+  for (int g = 0; g < G; ++g)
+    for (int h = g + 1; h < G; ++h)
+      if (l[g] == l[h]) Cc[((int64_t)u * G + g) * G + h] += 1;
+}
+
+/* Streaming sample + count over entries [first, first+count) without storing
+ * the lists (sizes far beyond host memory, e.g. sizeL = 1e9 or a 2^31 chunk
+ * crossing); OpenMP with per-thread histograms.  Returns invalid entries. */
+int64_t oracle_stream_counts(int n, uint64_t seed, uint64_t first, uint64_t count, int closed, int nfac0,
+                             const int32_t *desc0, const uint64_t *pat0, const uint64_t *apat0,
+                             const uint64_t *thr0, int nfac1, const int32_t *desc1, const uint64_t *pat1,
+                             const uint64_t *apat1, const uint64_t *thr1, int64_t *H, int64_t *Cc, int64_t *P) {
+  const prog_t p0 = {nfac0, desc0, pat0, apat0, thr0}, p1 = {nfac1, desc1, pat1, apat1, thr1};
+  const uint64_t t = perm_threshold(n);
+  const int w = 1 << n_qubits(n), G = n + 1;
+  const size_t hb = (size_t)w * G * w, cb = (size_t)w * G * G;
+  memset(H, 0, hb * sizeof(int64_t));
+  memset(Cc, 0, cb * sizeof(int64_t));
+  int64_t bad = 0;
+#pragma omp parallel
+  {
+    int64_t *h = calloc(hb, sizeof(int64_t)), *c = calloc(cb, sizeof(int64_t));
+    int64_t b = 0;
+    uint8_t vals[16];
+#pragma omp for schedule(static)
+    for (int64_t k = 0; k < (int64_t)count; ++k) {
+      entry_values(n, seed, first + (uint64_t)k, closed, &p0, &p1, t, vals);
+      count_values(vals, n, w, h, c, &b);
+    }
+#pragma omp critical
+    {
+      for (size_t i = 0; i < hb; ++i) H[i] += h[i];
+      for (size_t i = 0; i < cb; ++i) Cc[i] += c[i];
+      bad += b;
+    }
+    free(h);
+    free(c);
+  }
+  finalize(n, w, H, Cc, P);
+  return bad;
+}
+
+/* Batched independent instances (BASELINE configs[3]): instance i uses key
+ * seed_base + i over entries [0, count); counts per instance into
+ * H + i*w*G*w, Cc + i*w*G*G, P + i*w.  Parallel over instances. */
+void oracle_batched_counts(int n, uint64_t seed_base, int64_t n_inst, uint64_t count, int closed, int nfac0,
+                           const int32_t *desc0, const uint64_t *pat0, const uint64_t *apat0,
+                           const uint64_t *thr0, int nfac1, const int32_t *desc1, const uint64_t *pat1,
+                           const uint64_t *apat1, const uint64_t *thr1, int64_t *H, int64_t *Cc, int64_t *P) {
+  const prog_t p0 = {nfac0, desc0, pat0, apat0, thr0}, p1 = {nfac1, desc1, pat1, apat1, thr1};
+  const uint64_t t = perm_threshold(n);
+  const int w = 1 << n_qubits(n), G = n + 1;
+  const size_t hb = (size_t)w * G * w, cb = (size_t)w * G * G;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t i = 0; i < n_inst; ++i) {
+    int64_t *h = H + i * (int64_t)hb, *c = Cc + i * (int64_t)cb, *pp = P + i * (int64_t)w, b = 0;
+    memset(h, 0, hb * sizeof(int64_t));
+    memset(c, 0, cb * sizeof(int64_t));
+    uint8_t vals[16];
+    for (uint64_t k = 0; k < count; ++k) {
+      entry_values(n, seed_base + (uint64_t)i, k, closed, &p0, &p1, t, vals);
+      count_values(vals, n, w, h, c, &b);
+    }
+    finalize(n, w, h, c, pp);
+  }
+}
+
 int oracle_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

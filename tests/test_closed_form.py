@@ -159,3 +159,21 @@ def test_oracle_closed_statistics():
         cnt = np.bincount(L[g], minlength=16)
         chi2 = ((cnt - count / 16) ** 2 / (count / 16)).sum()
         assert chi2 < 60, (g, chi2)
+
+
+@pytest.mark.parametrize("n", [3, 7, 11])
+def test_oracle_stream_and_batched_counts(n):
+    """The streaming and batched count oracles (used as the checkers of the
+    full-size GPU tests) equal counts() over materialised lists."""
+    info = {"nfac": 0, "desc": np.zeros((0, 6), np.int32), "pat": np.zeros(1, np.uint64),
+            "apat": np.zeros(1, np.uint64), "thr": np.zeros(1, np.uint64)}
+    seed, first, count = 77 + n, (1 << 33) + 5, 20_003
+    L = oracle_lib.sample(n, seed, first, count, info, info, closed=True)
+    H, Cc, P, bad = oracle_lib.counts(L, n)
+    H2, C2, P2, bad2 = oracle_lib.stream_counts(n, seed, first, count, info, info, closed=True)
+    assert bad == bad2 == 0
+    assert np.array_equal(H, H2) and np.array_equal(Cc, C2) and np.array_equal(P, P2)
+    Hb, Cb, Pb = oracle_lib.batched_counts(n, 1000, 5, 3001, info, info, closed=True)
+    for i in range(5):
+        h, c, p, _ = oracle_lib.counts(oracle_lib.sample(n, 1000 + i, 0, 3001, info, info, closed=True), n)
+        assert np.array_equal(Hb[i], h) and np.array_equal(Cb[i], c) and np.array_equal(Pb[i], p)

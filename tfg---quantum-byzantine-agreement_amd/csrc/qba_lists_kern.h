@@ -27,6 +27,9 @@
 #ifndef QBA_QUAD_RANGE  // count: one range test per quad of entries (experiment builds: 0)
 #define QBA_QUAD_RANGE 1
 #endif
+#ifndef QBA_QTAB_MASK  // stage-table reads by the Q-correlated lanes only (experiment)
+#define QBA_QTAB_MASK 0
+#endif
 #ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
 #define QBA_NT_STORE 1
 #endif
@@ -533,8 +536,21 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
       uint4 A[4];
       uint2 sB[4];
       uint32_t sC[4];
+#if QBA_QTAB_MASK
+      // only Q-correlated lanes read the stage tables: half the lanes of each
+      // LDS read, so fewer bank conflicts (the not-Q lanes' values are
+      // discarded by qba_closed_finish's select)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        A[j] = make_uint4(0u, 0u, 0u, 0u);
+        sB[j] = make_uint2(0u, 0u);
+        sC[j] = 0u;
+        if (cl[j].w0 & 1u) qba_closed_tables<NP>(cl[j].rank, pl, A[j], sB[j], sC[j]);
+      }
+#else
 #pragma unroll
       for (int j = 0; j < 4; ++j) qba_closed_tables<NP>(cl[j].rank, pl, A[j], sB[j], sC[j]);
+#endif
 #pragma unroll
       for (int j = 0; j < 4; ++j) qba_closed_finish<NP>(cl[j], A[j], sB[j], sC[j], D[j]);
       return;
