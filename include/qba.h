@@ -148,9 +148,10 @@ QBA_API int qba_sample_check_batched(qba_ctx *ctx, int n_parties, uint64_t seed_
 QBA_API int qba_isq_indices(qba_ctx *ctx, const uint8_t *li_dev, const uint8_t *lc_dev, uint64_t count,
                     int64_t *idx_dev, int64_t cap, int64_t *count_host, qba_stream stream);
 /* P = {x in order : Lc[x] == v} keeping the order of `order` (tfg.py:182).
- * Synchronous. */
+ * Every index must lie in [0, lc_len) (QBA_EINVAL otherwise; nothing outside
+ * Lc is read).  Synchronous. */
 QBA_API int qba_select_eq(qba_ctx *ctx, const int64_t *order_dev, int64_t m, const uint8_t *lc_dev,
-                  int64_t v, int64_t *out_dev, int64_t *count_host, qba_stream stream);
+                  uint64_t lc_len, int64_t v, int64_t *out_dev, int64_t *count_host, qba_stream stream);
 /* tuple(Li[j] for j in P) in the given order (tfg.py:189, 291). */
 QBA_API int qba_gather(qba_ctx *ctx, const uint8_t *li_dev, uint64_t list_len, const int64_t *idx_dev,
                int64_t m, int64_t *out_dev, qba_stream stream);
@@ -160,11 +161,38 @@ QBA_API int qba_gather(qba_ctx *ctx, const uint8_t *li_dev, uint64_t list_len, c
 QBA_API int qba_consistent(qba_ctx *ctx, const int64_t *tuples_dev, int64_t m, int64_t len, int64_t v,
                    int64_t w, int32_t *ok_host, qba_stream stream);
 
+/* One received packet in ONE launch (tfg.py:189-192 in step 3a, 291-294 in
+ * step 3b): gathers the receiver's own tuple Li[j] for j in order (its set-
+ * iteration order of P) and evaluates Cond2/Cond3 of consistent(v, L | {own},
+ * w) (tfg.py:93-98) over the m received tuples of length len, with the set's
+ * de-duplication of own.  stage_dev = [order (len) | tuples (m x len)].
+ * out_dev (len + 3 + m int64): own tuple, then bad-index flag, received-
+ * tuple violation flag, own Cond2 violation flag, and per received tuple the
+ * number of positions equal to own; consistent <=> all flags 0 and every
+ * count in {0, len} (the host adds Cond1).  Asynchronous on `stream`. */
+QBA_API int qba_check_packet(qba_ctx *ctx, const uint8_t *li_dev, uint64_t list_len,
+                             const int64_t *stage_dev, int64_t m, int64_t len, int64_t v, int64_t w,
+                             int64_t *out_dev, qba_stream stream);
+
 /* ---- wire-compatible codec (rawS layout, tfg.py:81-84, 128-129, 142-161) -------- */
 QBA_API int qba_bits_to_values(qba_ctx *ctx, const int64_t *raw_dev, uint64_t count, int nq,
                        uint8_t *values_dev, qba_stream stream);
 QBA_API int qba_values_to_bits(qba_ctx *ctx, const uint8_t *values_dev, uint64_t count, int nq,
                        int64_t *raw_dev, qba_stream stream);
+
+/* ---- multi-GPU: the count all-reduce over RCCL ---------------- */
+/* The sizeL shards of one run live on G GPU-owner ranks; their int64 count
+ * buffers [H | C | P] are summed with ONE all-reduce.  This replaces nothing
+ * in tfg.py (the reference is single-process per party and never shards a
+ * list); it is what a non-torch caller (the mpiexec host) uses where the
+ * torch path calls torch.distributed.all_reduce.  Bootstrap: rank 0 calls
+ * qba_rccl_unique_id, ships the 128 bytes to the other owners (e.g. over
+ * MPI), every owner calls qba_rccl_init.  librccl is opened on first use;
+ * QBA_EUNSUPPORTED without it. */
+QBA_API int qba_rccl_unique_id(uint8_t *id_host /* [128] */);
+QBA_API int qba_rccl_init(qba_ctx *ctx, const uint8_t *id_host, int nranks, int rank);
+/* In place, sum over the communicator's ranks; asynchronous on `stream`. */
+QBA_API int qba_allreduce_i64(qba_ctx *ctx, int64_t *buf_dev, int64_t count, qba_stream stream);
 
 /* ---- helpers exported for tests ------------------------------------------------- */
 /* Vose alias table over k probabilities (host): thr[i] in [0, 2^32] (2^32 =

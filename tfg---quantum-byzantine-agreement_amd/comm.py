@@ -123,6 +123,8 @@ class Request:
 class LocalComm:
     """One rank's view of a :class:`LocalWorld` (the ``COMM_WORLD`` subset)."""
 
+    mpi = None  # set below: the in-process constants (LOCAL_MPI)
+
     def __init__(self, world: "LocalWorld", rank: int):
         self.world = world
         self.rank = rank
@@ -301,9 +303,114 @@ def local_mpi_module() -> types.ModuleType:
 
 
 def mpi_world():
-    """Return the real ``mpi4py.MPI`` module, or None when mpi4py is absent."""
+    """The MPI module of an ``mpiexec`` launch: ``mpi4py.MPI`` when it is
+    importable, else the ctypes MPICH binding (:mod:`.mpi`) when this process
+    is a rank of an mpiexec launch; None otherwise (use :class:`LocalWorld`)."""
     try:
         from mpi4py import MPI  # type: ignore
+        return MPI
     except ImportError:
+        pass
+    from . import mpi as mpi_ctypes
+    if not mpi_ctypes.launched_by_mpiexec():
         return None
+    try:
+        return mpi_ctypes.load()
+    except mpi_ctypes.MPIError:
+        return None
+
+
+# constants of the in-process world, as an MPI-module-like namespace
+LOCAL_MPI = types.SimpleNamespace(INT=INT, ANY_SOURCE=ANY_SOURCE, ANY_TAG=ANY_TAG, Status=Status)
+LocalComm.mpi = LOCAL_MPI
+
+
+def mpi_of(comm):
+    """The MPI namespace (INT, ANY_SOURCE, ANY_TAG, Status) that goes with a
+    communicator: the protocol must pass the datatypes and wildcards of the
+    library that owns the communicator (MPICH's ANY_SOURCE is -2, not -1)."""
+    ns = getattr(comm, "mpi", None)
+    if ns is not None:
+        return ns
+    from mpi4py import MPI  # type: ignore  # a real mpi4py communicator
     return MPI
+
+
+class EpochComm:
+    """Barrier-epoch delivery over a real MPI communicator.
+
+    The reference's rounds race: a rank still draining
+    ``Iprobe`` in round r can receive packets another rank sent in round r,
+    so outcomes under mpiexec depend on timing.  This wrapper gives a real
+    MPI run the same deterministic semantics as :class:`LocalWorld` (and as
+    the golden fixtures): every message carries its sender's epoch (number of
+    barriers passed) in the tag, ``tag + TAG_STRIDE * epoch``, and ``Iprobe``
+    reports only messages of earlier epochs, lowest (epoch, source) first;
+    within one (epoch, source) MPI's non-overtaking rule keeps the order.
+    Receives with an explicit tag after a probe use the probed message's
+    epoch; other explicit-tag receives the receiver's own (the protocol's
+    direct hand-offs happen inside one epoch).  Opt-in (``--rounds epoch``):
+    the default keeps the reference's own racy rounds."""
+
+    TAG_STRIDE = 256
+    HEAD_TAG = 1  # first message of every (P, v, L) packet (tfg.py:206)
+
+    def __init__(self, inner, count_traffic: bool = True):
+        self.inner = inner
+        self.epoch = 0
+        self._probed = {}
+        self.sent_messages = 0
+        self.sent_bytes = 0
+        self._count = count_traffic
+        m = mpi_of(inner)
+        self.mpi = types.SimpleNamespace(INT=m.INT, ANY_SOURCE=m.ANY_SOURCE, ANY_TAG=m.ANY_TAG, Status=m.Status)
+
+    def Get_rank(self) -> int:
+        return self.inner.Get_rank()
+
+    def Get_size(self) -> int:
+        return self.inner.Get_size()
+
+    def _tally(self, buf) -> None:
+        if self._count:
+            self.sent_messages += 1
+            self.sent_bytes += (buf[0] if isinstance(buf, (list, tuple)) else buf).nbytes
+
+    def Isend(self, buf, dest: int, tag: int = 0):
+        self._tally(buf)
+        return self.inner.Isend(buf, dest=dest, tag=tag + self.TAG_STRIDE * self.epoch)
+
+    def Send(self, buf, dest: int, tag: int = 0) -> None:
+        self._tally(buf)
+        self.inner.Send(buf, dest=dest, tag=tag + self.TAG_STRIDE * self.epoch)
+
+    def _tag(self, source, tag):
+        if tag == self.mpi.ANY_TAG:
+            return tag
+        return tag + self.TAG_STRIDE * self._probed.get(source, self.epoch)
+
+    def Irecv(self, buf, source=None, tag=None):
+        source = self.mpi.ANY_SOURCE if source is None else source
+        tag = self.mpi.ANY_TAG if tag is None else tag
+        return self.inner.Irecv(buf, source=source, tag=self._tag(source, tag))
+
+    def Recv(self, buf, source=None, tag=None, status=None) -> None:
+        source = self.mpi.ANY_SOURCE if source is None else source
+        tag = self.mpi.ANY_TAG if tag is None else tag
+        self.inner.Recv(buf, source=source, tag=self._tag(source, tag), status=status)
+
+    def Iprobe(self, source=None, tag=None, status=None) -> bool:
+        source = self.mpi.ANY_SOURCE if source is None else source
+        tag = self.HEAD_TAG if tag is None or tag == self.mpi.ANY_TAG else tag
+        srcs = range(self.Get_size()) if source == self.mpi.ANY_SOURCE else [source]
+        st = status if status is not None else self.mpi.Status()
+        for e in range(self.epoch):
+            for s in srcs:
+                if self.inner.Iprobe(source=s, tag=tag + self.TAG_STRIDE * e, status=st):
+                    self._probed[st.Get_source()] = e
+                    return True
+        return False
+
+    def Barrier(self) -> None:
+        self.inner.Barrier()
+        self.epoch += 1

@@ -30,8 +30,7 @@ from typing import Optional
 
 import numpy as np
 
-from . import comm as comm_mod
-from .protocol import INT, Party, _recv_array
+from .protocol import Party, _dt, _recv_array
 
 EMPTY = ()
 
@@ -104,11 +103,11 @@ class CountParty(Party):
             self.say("|W| =", self.w)
             flat = self.engine.count_tables(n, self.sizeL, self.seed, self.inject, self.chunk)
             self.tables = CountTables(n, flat)
-            reqs = [c.Isend([self.tables.flat, INT], dest=r) for r in range(1, n + 1)]
+            reqs = [c.Isend([self.tables.flat, _dt(c)], dest=r) for r in range(1, n + 1)]
             for r in reqs:
                 r.Wait()
             return
-        self.tables = CountTables(n, _recv_array(c, 0, comm_mod.ANY_TAG, size))
+        self.tables = CountTables(n, _recv_array(c, 0, None, size))
 
     def commander_setup(self):
         self.v = self.rng.randint(self.w)
@@ -121,19 +120,18 @@ class CountParty(Party):
         return self.tables.desc(self.rank, P.u)
 
     def check(self, v, L) -> bool:
-        ok = self.tables.consistent(v, L)
-        if ok:
-            self.stats.accept += 1
-        else:
-            self.stats.reject += 1
-        return ok
+        return self._tally(self.tables.consistent(v, L))
+
+    def add_own_and_check(self, P, v, L) -> bool:
+        L.add(self.own_tuple(P))
+        return self.check(v, L)
 
     def send(self, dest, P, v, L):
         self.stats.sent += 1
         pairs = np.array([x for d in L for x in (d if d != EMPTY else (-1, -1))], dtype=np.int64)
         head = np.array([-1 if P.u is None else P.u, int(v), len(L)], dtype=np.int64)
-        self.comm.Isend([head, INT], dest=dest, tag=1).Wait()
-        self.comm.Isend([pairs, INT], dest=dest, tag=2).Wait()
+        self.comm.Isend([head, _dt(self.comm)], dest=dest, tag=1).Wait()
+        self.comm.Isend([pairs, _dt(self.comm)], dest=dest, tag=2).Wait()
 
     def recv(self, src):
         head = _recv_array(self.comm, src, 1, 3)

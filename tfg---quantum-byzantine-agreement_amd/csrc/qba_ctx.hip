@@ -59,6 +59,7 @@ extern "C" int qba_init(int device, qba_ctx **out) {
 extern "C" int qba_destroy(qba_ctx *ctx) {
   if (!ctx) return QBA_OK;
   (void)hipSetDevice(ctx->device);
+  qba_rccl_release(ctx);
   for (int n = 0; n <= QBA_MAX_PARTIES; ++n) {
     if (ctx->prog_dev[n]) (void)hipFree(ctx->prog_dev[n]);
     free(ctx->prog_host[n]);

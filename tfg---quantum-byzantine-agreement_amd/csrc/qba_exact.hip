@@ -51,22 +51,41 @@ extern "C" int qba_isq_indices(qba_ctx *ctx, const uint8_t *li, const uint8_t *l
 }
 
 // --- P = {x in isQCorr : Lc[x] == v}, isQCorr's iteration order kept (tfg.py:182) ------
+// An index outside [0, lc_len) is never dereferenced: it flags the call,
+// which then fails with QBA_EINVAL (the order comes through the public ABI).
 struct QbaSelPred {
   const int64_t *order;
   const uint8_t *lc;
+  uint64_t lc_len;
   int64_t v;
   int64_t *out;
-  __device__ bool test(int64_t i) const { return (int64_t)lc[order[i]] == v; }
+  int32_t *bad;
+  __device__ bool test(int64_t i) const {
+    const int64_t x = order[i];
+    if ((uint64_t)x >= lc_len) {
+      atomicOr(bad, 1);
+      return false;
+    }
+    return (int64_t)lc[x] == v;
+  }
   __device__ void emit(int64_t i, int64_t pos) const { out[pos] = order[i]; }
 };
 
 extern "C" int qba_select_eq(qba_ctx *ctx, const int64_t *order, int64_t m, const uint8_t *lc,
-                             int64_t v, int64_t *out, int64_t *count_host, qba_stream stream) {
+                             uint64_t lc_len, int64_t v, int64_t *out, int64_t *count_host,
+                             qba_stream stream) {
   if (!ctx || !count_host || m < 0 || (m && (!order || !lc || !out)))
     return qba_fail(QBA_EINVAL, "qba_select_eq: bad arguments");
   int rc = qba_set_device(ctx);
   if (rc) return rc;
-  return qba_compact(ctx, QbaSelPred{order, lc, v, out}, m, m, count_host, (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  QBA_HIP(hipMemsetAsync(ctx->flag, 0, sizeof(int32_t), s));
+  rc = qba_compact(ctx, QbaSelPred{order, lc, lc_len, v, out, ctx->flag}, m, m, count_host, s);
+  if (rc) return rc;
+  int32_t bad = 0;  // qba_compact has synchronised the stream
+  QBA_HIP(hipMemcpy(&bad, ctx->flag, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (bad) return qba_fail(QBA_EINVAL, "qba_select_eq: index outside Lc");
+  return QBA_OK;
 }
 
 // --- tuple(Li[j] for j in P)  (tfg.py:189, 291) --------------------------------------
@@ -141,6 +160,60 @@ extern "C" int qba_consistent(qba_ctx *ctx, const int64_t *tuples, int64_t m, in
   }
   QBA_HIP(hipMemcpyAsync(ok_host, ctx->flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   QBA_HIP(hipStreamSynchronize(s));
+  return QBA_OK;
+}
+
+// --- one packet of the exact-order protocol in ONE launch (tfg.py:189-192, 291-294) ---
+// The receiving lieutenant gathers its own tuple Li[P] in its set-iteration
+// order and evaluates consistent(v, L | {own}) (tfg.py:87-98) over the packet's
+// m received tuples.  Cond1 (equal lengths) is the host's; here all tuples
+// have length len.  L is a set, so own is dropped from the pairwise test when
+// it equals a received tuple: per received tuple a, eq[a] counts positions k
+// with t_a[k] == own[k], and a pair (a, own) violates Cond3 iff
+// 0 < eq[a] < len.  Output (device, int64): own[0..len), then
+// [len] bad index, [len+1] Cond2/3 violation among the received tuples,
+// [len+2] Cond2 violation of own, [len+3+a] eq[a].
+__global__ void qba_k_check_packet(const uint8_t *__restrict__ li, uint64_t list_len,
+                                   const int64_t *__restrict__ stage, int64_t m, int64_t len, int64_t v,
+                                   int64_t w, int64_t *__restrict__ out) {
+  const int64_t *order = stage, *t = stage + len;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < len;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = order[k];
+    int64_t own = -1;
+    if ((uint64_t)j >= list_len) {
+      atomicOr(reinterpret_cast<unsigned long long *>(&out[len]), 1ull);
+    } else {
+      own = li[j];
+    }
+    out[k] = own;
+    if (own < 0 || own > w || own == v) atomicOr(reinterpret_cast<unsigned long long *>(&out[len + 2]), 1ull);
+    bool good = true;
+    for (int64_t a = 0; a < m; ++a) {
+      const int64_t x = t[a * len + k];
+      if (x < 0 || x > w || x == v) good = false;
+      for (int64_t b = a + 1; b < m && good; ++b)
+        if (t[b * len + k] == x) good = false;
+      if (x == own) atomicAdd(reinterpret_cast<unsigned long long *>(&out[len + 3 + a]), 1ull);
+    }
+    if (!good) atomicOr(reinterpret_cast<unsigned long long *>(&out[len + 1]), 1ull);
+  }
+}
+
+extern "C" int qba_check_packet(qba_ctx *ctx, const uint8_t *li, uint64_t list_len, const int64_t *stage,
+                                int64_t m, int64_t len, int64_t v, int64_t w, int64_t *out,
+                                qba_stream stream) {
+  if (!ctx || !out || m < 0 || len < 0 || (len && (!li || !stage)))
+    return qba_fail(QBA_EINVAL, "qba_check_packet: bad arguments");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  QBA_HIP(hipMemsetAsync(out + len, 0, (size_t)(3 + m) * sizeof(int64_t), s));
+  if (len > 0) {
+    const unsigned grid = (unsigned)std::min<int64_t>((len + 255) / 256, 1024);
+    hipLaunchKernelGGL(qba_k_check_packet, dim3(grid), dim3(256), 0, s, li, list_len, stage, m, len, v, w, out);
+    QBA_HIP(hipGetLastError());
+  }
   return QBA_OK;
 }
 

@@ -157,7 +157,11 @@ struct qba_ctx {
   int64_t *count1 = nullptr; // 1-word device counter
   int64_t *stats = nullptr;  // [2]: last counts launch: Q entries with a value >= w, spare
   uint64_t chunk = QBA_CHUNK;  // entries per list-kernel launch (env QBA_CHUNK_ENTRIES, tests)
+  // RCCL communicator of the GPU-owner ranks (qba_rccl_init), or null
+  void *rccl_comm = nullptr;
+  int rccl_ranks = 0;
 };
+void qba_rccl_release(qba_ctx *ctx);
 
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes);
 int qba_ensure_scan(qba_ctx *ctx, size_t bytes);

@@ -215,10 +215,12 @@ class Engine:
         return counts
 
     def count_tables(self, n: int, sizeL: int, seed: int = 0, lists: Optional[np.ndarray] = None,
-                     chunk: int = 1 << 27) -> np.ndarray:
-        """Flat int64 [H | C | P] over sizeL entries: injected host lists are
-        checked on the device, otherwise entries are sampled and checked in
-        chunks of `chunk` (lists are written once to a reused buffer)."""
+                     chunk: int = 1 << 27, first: int = 0, device_out: bool = False):
+        """Flat int64 [H | C | P] over entries [first, first + sizeL): injected
+        host lists (shape (n+1, sizeL)) are checked on the device, otherwise
+        entries are sampled and checked in chunks of `chunk` (lists are written
+        once to a reused buffer).  device_out returns the device tensor (for a
+        collective) instead of a host copy."""
         self._check_n(n)
         _, w = self.sizes(n)
         g = n + 1
@@ -234,14 +236,13 @@ class Engine:
             self.check_counts(dev, n, sizeL, counts)
         else:
             buf = self.alloc_lists(n, min(chunk, max(sizeL, 1)))
-            for first in range(0, sizeL, chunk):
-                self.sample_check(n, seed, first, min(chunk, sizeL - first), buf, counts,
-                                  accumulate=first > 0)
-        out = flat.cpu().numpy()
+            for off in range(0, sizeL, chunk):
+                self.sample_check(n, seed, first + off, min(chunk, sizeL - off), buf, counts,
+                                  accumulate=off > 0)
         if sizeL and self.last_stats()[0] != 0:
             raise QbaError("lists hold values >= w at Q-correlated positions: count mode "
                            "cannot evaluate them (the reference never produces such lists)")
-        return out
+        return flat if device_out else flat.cpu().numpy()
 
     def last_stats(self) -> np.ndarray:
         out = np.zeros(2, np.int64)
@@ -276,7 +277,7 @@ class Engine:
         d_order = self.to_device(np.asarray(order, dtype=np.int64))
         out = torch.empty(m, dtype=torch.int64, device=self.device)
         found = C.c_int64()
-        call("qba_select_eq", self.ctx, _ptr(d_order), m, _ptr(lc), int(v), _ptr(out),
+        call("qba_select_eq", self.ctx, _ptr(d_order), m, _ptr(lc), lc.numel(), int(v), _ptr(out),
              C.byref(found), self.stream())
         return out[: found.value].cpu().numpy()
 
@@ -289,6 +290,63 @@ class Engine:
         out = torch.empty(m, dtype=torch.int64, device=self.device)
         call("qba_gather", self.ctx, _ptr(li), li.numel(), _ptr(d_idx), m, _ptr(out), self.stream())
         return out.cpu().numpy()
+
+    def _staging(self, n_stage: int, n_out: int):
+        """Reusable pinned host / device staging for check_packet (grown on demand)."""
+        if getattr(self, "_st_cap", (0, 0))[0] < n_stage or self._st_cap[1] < n_out:
+            cs, co = max(n_stage, 4096), max(n_out, 4096)
+            self._st_h = torch.empty(cs, dtype=torch.int64).pin_memory()
+            self._st_d = torch.empty(cs, dtype=torch.int64, device=self.device)
+            self._out_h = torch.empty(co, dtype=torch.int64).pin_memory()
+            self._out_d = torch.empty(co, dtype=torch.int64, device=self.device)
+            self._st_cap = (cs, co)
+        return self._st_h, self._st_d, self._out_h, self._out_d
+
+    def check_packet(self, li: torch.Tensor, order: np.ndarray, rows: Sequence[Sequence[int]], v: int,
+                     w: int) -> Tuple[tuple, bool]:
+        """One packet of the exact-order protocol (tfg.py:189-192, 291-294):
+        own = tuple(Li[j] for j in order) and Cond2/Cond3 of
+        consistent(v, rows | {own}, w), in one launch and one host sync.  All
+        rows must have len(order) entries (Cond1 stays with the caller)."""
+        ln, m = len(order), len(rows)
+        st_h, st_d, out_h, out_d = self._staging(ln * (m + 1), ln + 3 + m)
+        hv = st_h.numpy()
+        hv[:ln] = order
+        if m and ln:
+            hv[ln:ln * (m + 1)] = np.asarray(rows, dtype=np.int64).reshape(-1)
+        n_st, n_out = ln * (m + 1), ln + 3 + m
+        stream = torch.cuda.current_stream(self.device)
+        if n_st:
+            st_d[:n_st].copy_(st_h[:n_st], non_blocking=True)
+        call("qba_check_packet", self.ctx, _ptr(li), li.numel(), _ptr(st_d), m, ln, int(v), int(w),
+             _ptr(out_d), self.stream())
+        out_h[:n_out].copy_(out_d[:n_out], non_blocking=True)
+        stream.synchronize()
+        o = out_h[:n_out].numpy()
+        if o[ln]:
+            raise QbaError("qba_check_packet: index outside the list")
+        eq = o[ln + 3:]
+        ok = not o[ln + 1] and not o[ln + 2] and bool(np.all((eq == 0) | (eq == ln)))
+        if m and not ln:  # every tuple empty: the set is {()}, vacuously consistent
+            ok = True
+        return tuple(o[:ln].tolist()), ok
+
+    def allreduce_i64(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over the RCCL communicator of rccl_init (qba_allreduce_i64)."""
+        if t.dtype != torch.int64 or not t.is_contiguous() or t.device != self.device:
+            raise QbaError("allreduce_i64 needs a contiguous int64 tensor on this engine's device")
+        call("qba_allreduce_i64", self.ctx, _ptr(t), t.numel(), self.stream())
+        return t
+
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        call("qba_rccl_unique_id", buf)
+        return bytes(buf)
+
+    def rccl_init(self, uid: bytes, nranks: int, rank: int) -> None:
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        call("qba_rccl_init", self.ctx, buf, nranks, rank)
 
     def consistent_rows(self, rows: np.ndarray, v: int, w: int) -> bool:
         """Cond2 and Cond3 of tfg.py:93-98 over an (m, len) int64 matrix."""

@@ -37,8 +37,10 @@ import numpy as np
 from . import comm as comm_mod
 from .resource import n_qubits
 
-INT = comm_mod.INT
-ANY_SOURCE = comm_mod.ANY_SOURCE
+
+def _dt(comm):
+    """MPI INT of the library that owns `comm` (tfg.py:110 declares MPI.INT)."""
+    return comm_mod.mpi_of(comm).INT
 
 
 # ---------------------------------------------------------------------------
@@ -60,10 +62,11 @@ def generacionListas(nParties, size, nQubits, w, engine=None, seed=0, lists=None
         if arr.shape != (nParties + 1, size):
             raise ValueError(f"injected lists must have shape {(nParties + 1, size)}")
         dev = engine.to_device(arr)
-    out = np.empty((nParties + 1, nQubits * size), np.int64)
-    for g in range(nParties + 1):
-        out[g] = engine.to_host(engine.values_to_bits(dev[g, :size], size, nQubits))
-    return out
+    rows = [engine.values_to_bits(dev[g, :size], size, nQubits) for g in range(nParties + 1)]
+    if hasattr(rows[0], "new_empty"):  # device tensors: one stack, one copy to the host
+        import torch
+        return engine.to_host(torch.stack(rows))
+    return np.stack([engine.to_host(r) for r in rows])
 
 
 def measure_to_ints(raw, sizeL, nQubits, engine=None):
@@ -108,7 +111,8 @@ def send_pvl(comm, rank, dest, P, v, L, is_biz, log=None):
     for sub in L:
         msgs.append(np.array(len(sub), dtype=np.int64))
         msgs.append(np.array(sub, dtype=np.int64))
-    reqs = [comm.Isend([m, INT], dest=dest, tag=t) for t, m in enumerate(msgs, start=1)]
+    dt = _dt(comm)
+    reqs = [comm.Isend([m, dt], dest=dest, tag=t) for t, m in enumerate(msgs, start=1)]
     for r in reqs:
         r.Wait()
     if log:
@@ -116,8 +120,10 @@ def send_pvl(comm, rank, dest, P, v, L, is_biz, log=None):
 
 
 def _recv_array(comm, src, tag, n):
+    """Receive n int64 from src; tag None = ANY_TAG of the comm's library."""
     buf = np.empty(n, dtype=np.int64)
-    comm.Irecv([buf, INT], source=src, tag=tag).Wait()
+    mpi = comm_mod.mpi_of(comm)
+    comm.Irecv([buf, mpi.INT], source=src, tag=mpi.ANY_TAG if tag is None else tag).Wait()
     return buf
 
 
@@ -196,12 +202,12 @@ class Party:
         c, n = self.comm, self.n
         if self.rank == 0:
             ids = self.rng.choice(np.arange(1, n + 1), self.n_dis, replace=False)
-            reqs = [c.Isend([np.array(i in ids, dtype=np.int64), INT], dest=i) for i in range(1, n + 1)]
+            reqs = [c.Isend([np.array(i in ids, dtype=np.int64), _dt(c)], dest=i) for i in range(1, n + 1)]
             for r in reqs:
                 r.Wait()
             self.dishonest_ids = ids
             return ids
-        self.dishonest = bool(_recv_array(c, 0, comm_mod.ANY_TAG, 1)[0])
+        self.dishonest = bool(_recv_array(c, 0, None, 1)[0])
         self.say(f"[{self.rank}] I'm {'dis' if self.dishonest else ''}honest")
         return self.dishonest
 
@@ -211,16 +217,16 @@ class Party:
         if self.rank == 0:
             self.say("|W| =", self.w)
             raw = generacionListas(n, sl, nq, self.w, self.engine, self.seed, self.inject)
-            reqs = [c.Isend([raw[0], INT], dest=1)]
-            reqs += [c.Isend([raw[g], INT], dest=g) for g in range(1, n + 1)]
+            reqs = [c.Isend([raw[0], _dt(c)], dest=1)]
+            reqs += [c.Isend([raw[g], _dt(c)], dest=g) for g in range(1, n + 1)]
             for r in reqs:
                 r.Wait()
             return
         mine = np.empty(nq * sl, np.int64)
-        req = c.Irecv([mine, INT], source=0)  # posted first: gets rawS[0] at rank 1
+        req = c.Irecv([mine, _dt(c)], source=0)  # posted first: gets rawS[0] at rank 1
         if self.rank == 1:
             extra = np.empty(nq * sl, np.int64)
-            c.Irecv([extra, INT], source=0).Wait()
+            c.Irecv([extra, _dt(c)], source=0).Wait()
             self.lc = self._decode(extra)
         req.Wait()
         self.li = self._decode(mine)
@@ -250,11 +256,30 @@ class Party:
 
     def check(self, v, L) -> bool:
         ok = consistent(v, L, self.w, self.engine)
+        return self._tally(ok)
+
+    def _tally(self, ok: bool) -> bool:
         if ok:
             self.stats.accept += 1
         else:
             self.stats.reject += 1
         return ok
+
+    def add_own_and_check(self, P, v, L) -> bool:
+        """``L.add(tuple(Li[j] for j in P))`` then ``consistent(v, L, w)``
+        (tfg.py:189-192, 291-294): the gather and Cond2/Cond3 run as ONE
+        device launch with one host sync (qba_check_packet); Cond1 and the
+        set bookkeeping stay here."""
+        fast = getattr(self.engine, "check_packet", None)
+        if fast is None:  # engines without the fused call (the CPU test engine)
+            L.add(self.own_tuple(P))
+            return self.check(v, L)
+        order = np.fromiter(P, dtype=np.int64, count=len(P))
+        received = list(L)
+        same_len = all(len(t) == len(order) for t in received)
+        own, ok = fast(self.li, order, received if same_len else [], v, self.w)
+        L.add(own)
+        return self._tally(ok and same_len)
 
     def send(self, dest, P, v, L):
         self.stats.sent += 1
@@ -278,9 +303,9 @@ class Party:
                 self.send(dest, self.p_for(v), v, set())
         elif self.rank > 1:
             P, v, L = self.recv(1)
-            L.add(self.own_tuple(P))
+            ok = self.add_own_and_check(P, v, L)
             self.say(f"[{self.rank}] L = {L}")
-            if self.check(v, L):
+            if ok:
                 self.Vi.add(v)
                 self.lieu_broadcast(P, v, L)
 
@@ -309,8 +334,7 @@ class Party:
 
     # tfg.py:289-300
     def lieu_receive(self, P, v, L, rnd):
-        L.add(self.own_tuple(P))
-        if self.check(v, L) and v not in self.Vi and len(L) == rnd + 1:
+        if self.add_own_and_check(P, v, L) and v not in self.Vi and len(L) == rnd + 1:
             self.Vi.add(v)
             if rnd <= self.n_dis:
                 self.lieu_broadcast(P, v, L)
@@ -325,11 +349,12 @@ class Party:
             self.commander_setup()
         self.comm_broadcast()
         c.Barrier()
-        status = comm_mod.Status() if isinstance(c, comm_mod.LocalComm) else _mpi_status(c)
+        mpi = comm_mod.mpi_of(c)
+        status = mpi.Status()
         for rnd in range(1, self.n_dis + 2):
             if self.rank > 1:
                 inbox = []
-                while c.Iprobe(source=ANY_SOURCE, status=status):
+                while c.Iprobe(source=mpi.ANY_SOURCE, status=status):
                     inbox.append(self.recv(status.Get_source()))
                 for P, v, L in inbox:
                     self.lieu_receive(P, v, L, rnd)
@@ -343,11 +368,11 @@ class Party:
                 if not self.tolerate_empty_vi:
                     raise
                 self.empty_vi_error, d = True, -1
-            c.Send([np.array(d, dtype=np.int64), INT], dest=0)
+            c.Send([np.array(d, dtype=np.int64), _dt(c)], dest=0)
             return None
         result = np.empty(self.n, dtype=np.int64)
         for src in range(1, self.n + 1):
-            result[src - 1] = _recv_array(c, src, comm_mod.ANY_TAG, 1)[0]
+            result[src - 1] = _recv_array(c, src, None, 1)[0]
         ids = self.dishonest_ids
         honest = {int(result[i]) for i in range(self.n) if i + 1 not in ids}
         self.say("Decisions:", result)
@@ -355,11 +380,6 @@ class Party:
         self.say("Success:", len(honest) == 1)
         return {"decisions": result.tolist(), "dishonest": sorted(int(x) for x in ids),
                 "success": len(honest) == 1}
-
-
-def _mpi_status(c):
-    from mpi4py import MPI  # type: ignore  # noqa: F401  (real MPI only)
-    return MPI.Status()
 
 
 def QBA(sizeL, nDishonest, engine=None, comm=None, rng=None, log=print, lists=None, seed=0):
@@ -372,7 +392,7 @@ def QBA(sizeL, nDishonest, engine=None, comm=None, rng=None, log=print, lists=No
     if comm is None:
         mpi = comm_mod.mpi_world()
         if mpi is None:
-            raise RuntimeError("mpi4py is not installed: use run_local() for an in-process run")
+            raise RuntimeError("not an mpiexec launch (and no mpi4py): use run_local() for an in-process run")
         comm = mpi.COMM_WORLD
     party = Party(comm, sizeL, nDishonest, engine, rng if rng is not None else np.random, log, lists, seed)
     return party.run()

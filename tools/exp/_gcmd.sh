@@ -1,4 +1,3 @@
 set -eo pipefail
-mkdir -p gpurun_out/ab1
-timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab1/pytest.log 2>&1
-bash tools/exp/ab.sh ab1
+mkdir -p gpurun_out/wl1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_workloads.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/wl1/pytest.log 2>&1
