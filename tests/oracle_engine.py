@@ -35,8 +35,12 @@ class OracleEngine:
     def consistent_rows(self, rows, v, w):
         return orc.consistent(v, {tuple(r) for r in rows.tolist()}, w) if len(rows) else True
 
-    def count_tables(self, n, sizeL, seed=0, lists=None, chunk=None):
-        if lists is None:
-            raise NotImplementedError("the oracle engine only checks injected lists")
-        H, C, P = orc.counts(np.asarray(lists), n)
+    def count_tables(self, n, sizeL, seed=0, lists=None, chunk=None, first=0, device_out=False):
+        if lists is None:  # sampled: the C twin's closed-form schedule (n <= 11)
+            import oracle_lib
+            dummy = {"nfac": 0, "desc": np.zeros((0, 6), np.int32), "pat": np.zeros(1, np.uint64),
+                     "apat": np.zeros(1, np.uint64), "thr": np.zeros(1, np.uint64)}
+            H, C, P, bad = oracle_lib.stream_counts(n, seed, first, sizeL, dummy, dummy, closed=True)
+        else:
+            H, C, P = orc.counts(np.asarray(lists), n)
         return np.concatenate([H.ravel(), C.ravel(), P.ravel()])

