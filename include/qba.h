@@ -174,11 +174,26 @@ QBA_API int qba_check_packet(qba_ctx *ctx, const uint8_t *li_dev, uint64_t list_
                              const int64_t *stage_dev, int64_t m, int64_t len, int64_t v, int64_t w,
                              int64_t *out_dev, qba_stream stream);
 
+/* Synchronous host-pointer form of qba_check_packet (the protocol's
+ * per-packet call: one H2D through the context's pinned staging, one launch,
+ * one D2H, one sync).  stage_host / out_host as above, in host memory. */
+QBA_API int qba_check_packet_host(qba_ctx *ctx, const uint8_t *li_dev, uint64_t list_len,
+                                  const int64_t *stage_host, int64_t m, int64_t len, int64_t v, int64_t w,
+                                  int64_t *out_host, qba_stream stream);
+
 /* ---- wire-compatible codec (rawS layout, tfg.py:81-84, 128-129, 142-161) -------- */
 QBA_API int qba_bits_to_values(qba_ctx *ctx, const int64_t *raw_dev, uint64_t count, int nq,
                        uint8_t *values_dev, qba_stream stream);
 QBA_API int qba_values_to_bits(qba_ctx *ctx, const uint8_t *values_dev, uint64_t count, int nq,
                        int64_t *raw_dev, qba_stream stream);
+/* rawS of a run (tfg.py:81-84, as rank 0 ships it at tfg.py:142-145): rows
+ * [0, rows) of a lists matrix encoded to raw_host[rows][count*nq].  Sync. */
+QBA_API int qba_lists_to_bits_host(qba_ctx *ctx, const uint8_t *lists_dev, uint64_t ld, int rows,
+                                   uint64_t count, int nq, int64_t *raw_host, qba_stream stream);
+/* measure_to_ints of a received row (tfg.py:158, 161) straight from the
+ * receive buffer in host memory to a device list.  Synchronous. */
+QBA_API int qba_bits_to_values_host(qba_ctx *ctx, const int64_t *raw_host, uint64_t count, int nq,
+                                    uint8_t *values_dev, qba_stream stream);
 
 /* ---- multi-GPU: the count all-reduce over RCCL ---------------- */
 /* The sizeL shards of one run live on G GPU-owner ranks; their int64 count

@@ -46,6 +46,9 @@ SIGNATURES = {
     "qba_isq_indices": [_p, _p, _p, _u64, _p, _i64, _pi64, _p],
     "qba_select_eq": [_p, _p, _i64, _p, _u64, _i64, _p, _pi64, _p],
     "qba_check_packet": [_p, _p, _u64, _p, _i64, _i64, _i64, _i64, _p, _p],
+    "qba_check_packet_host": [_p, _p, _u64, _p, _i64, _i64, _i64, _i64, _p, _p],
+    "qba_lists_to_bits_host": [_p, _p, _u64, C.c_int, _u64, C.c_int, _p, _p],
+    "qba_bits_to_values_host": [_p, _p, _u64, C.c_int, _p, _p],
     "qba_rccl_unique_id": [_p],
     "qba_rccl_init": [_p, _p, C.c_int, C.c_int],
     "qba_allreduce_i64": [_p, _p, _i64, _p],

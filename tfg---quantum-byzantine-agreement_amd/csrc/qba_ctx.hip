@@ -69,6 +69,8 @@ extern "C" int qba_destroy(qba_ctx *ctx) {
   if (ctx->flag) (void)hipFree(ctx->flag);
   if (ctx->count1) (void)hipFree(ctx->count1);
   if (ctx->stats) (void)hipFree(ctx->stats);
+  if (ctx->pin_h) (void)hipHostFree(ctx->pin_h);
+  if (ctx->pin_d) (void)hipFree(ctx->pin_d);
   delete ctx;
   return QBA_OK;
 }
@@ -90,6 +92,21 @@ static int ensure(void *&ptr, size_t &have, size_t want, const char *what) {
 
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes) { return ensure(ctx->slab, ctx->slab_bytes, bytes, "slab"); }
 int qba_ensure_scan(qba_ctx *ctx, size_t bytes) { return ensure(ctx->scan, ctx->scan_bytes, bytes, "scan"); }
+
+// pinned host staging (hipHostMalloc) + device staging for the synchronous
+// host-pointer entry points: one H2D, the kernel(s), one D2H, one sync.
+int qba_ensure_staging(qba_ctx *ctx, size_t host_bytes, size_t dev_bytes) {
+  if (ctx->pin_h_bytes < host_bytes) {
+    if (ctx->pin_h) QBA_HIP(hipHostFree(ctx->pin_h));
+    ctx->pin_h = nullptr;
+    ctx->pin_h_bytes = 0;
+    const size_t sz = host_bytes + host_bytes / 4 + 65536;
+    if (hipHostMalloc(&ctx->pin_h, sz, hipHostMallocDefault) != hipSuccess)
+      return qba_fail(QBA_ENOMEM, "pinned staging allocation failed");
+    ctx->pin_h_bytes = sz;
+  }
+  return ensure(ctx->pin_d, ctx->pin_d_bytes, dev_bytes, "device staging");
+}
 
 extern "C" int qba_last_stats(qba_ctx *ctx, int64_t *out2) {
   if (!ctx || !out2) return qba_fail(QBA_EINVAL, "qba_last_stats: bad arguments");

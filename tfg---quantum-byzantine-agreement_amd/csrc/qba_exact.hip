@@ -5,6 +5,8 @@
 // (tfg.py:189, 291) and compares tuples position by position (tfg.py:97-98),
 // so parity with it needs the host's index orders, not a canonical one.  The
 // host keeps the Python sets; these kernels do the per-element work.
+#include <string.h>
+
 #include "qba_compact.h"
 
 __global__ void __launch_bounds__(1024)
@@ -217,6 +219,32 @@ extern "C" int qba_check_packet(qba_ctx *ctx, const uint8_t *li, uint64_t list_l
   return QBA_OK;
 }
 
+// Synchronous host-pointer form (the protocol host's per-packet call): the
+// stage goes through the ctx's pinned staging, the result comes back to
+// out_host; one H2D, one launch, one D2H, one stream sync.
+extern "C" int qba_check_packet_host(qba_ctx *ctx, const uint8_t *li, uint64_t list_len,
+                                     const int64_t *stage_host, int64_t m, int64_t len, int64_t v,
+                                     int64_t w, int64_t *out_host, qba_stream stream) {
+  if (!ctx || !out_host || m < 0 || len < 0 || (len && (!li || !stage_host)))
+    return qba_fail(QBA_EINVAL, "qba_check_packet_host: bad arguments");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  const size_t nin = (size_t)len * (size_t)(m + 1), nout = (size_t)(len + 3 + m);
+  if ((rc = qba_ensure_staging(ctx, 8 * (nin > nout ? nin : nout), 8 * (nin + nout)))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  int64_t *pin = static_cast<int64_t *>(ctx->pin_h), *d_in = static_cast<int64_t *>(ctx->pin_d),
+          *d_out = d_in + nin;
+  if (nin) {
+    memcpy(pin, stage_host, 8 * nin);
+    QBA_HIP(hipMemcpyAsync(d_in, pin, 8 * nin, hipMemcpyHostToDevice, s));
+  }
+  if ((rc = qba_check_packet(ctx, li, list_len, d_in, m, len, v, w, d_out, stream))) return rc;
+  QBA_HIP(hipMemcpyAsync(pin, d_out, 8 * nout, hipMemcpyDeviceToHost, s));
+  QBA_HIP(hipStreamSynchronize(s));
+  memcpy(out_host, pin, 8 * nout);
+  return QBA_OK;
+}
+
 // --- wire codec: rawS bits (one int64 per measured bit, MSB first) <-> values ---------
 __global__ void qba_k_bits_to_values(const int64_t *__restrict__ raw, uint64_t count, int nq,
                                      uint8_t *__restrict__ vals) {
@@ -249,6 +277,52 @@ extern "C" int qba_bits_to_values(qba_ctx *ctx, const int64_t *raw, uint64_t cou
   hipLaunchKernelGGL(qba_k_bits_to_values, dim3(grid), dim3(256), 0, (hipStream_t)stream, raw,
                      count, nq, vals);
   QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}
+
+// rawS of a whole run (tfg.py:81-84): rows [0, rows) of a lists matrix (row
+// stride ld) encoded and copied to raw_host[rows][count * nq]; synchronous.
+extern "C" int qba_lists_to_bits_host(qba_ctx *ctx, const uint8_t *lists, uint64_t ld, int rows,
+                                      uint64_t count, int nq, int64_t *raw_host, qba_stream stream) {
+  if (!ctx || rows < 0 || nq < 1 || nq > 8 || (rows && count && (!lists || !raw_host)))
+    return qba_fail(QBA_EINVAL, "qba_lists_to_bits_host: bad arguments");
+  const size_t n = (size_t)rows * count * nq;
+  if (n == 0) return QBA_OK;
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  if ((rc = qba_ensure_staging(ctx, 8 * n, 8 * n))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  int64_t *d = static_cast<int64_t *>(ctx->pin_d);
+  const unsigned grid = (unsigned)std::min<uint64_t>((count * nq + 255) / 256, 8192);
+  for (int g = 0; g < rows; ++g)
+    hipLaunchKernelGGL(qba_k_values_to_bits, dim3(grid), dim3(256), 0, s, lists + (uint64_t)g * ld, count, nq,
+                       d + (size_t)g * count * nq);
+  QBA_HIP(hipGetLastError());
+  QBA_HIP(hipMemcpyAsync(ctx->pin_h, d, 8 * n, hipMemcpyDeviceToHost, s));
+  QBA_HIP(hipStreamSynchronize(s));
+  memcpy(raw_host, ctx->pin_h, 8 * n);
+  return QBA_OK;
+}
+
+// measure_to_ints of a received rawS row (tfg.py:158, 161) from host memory:
+// one H2D through the pinned staging, the decode kernel; synchronous.
+extern "C" int qba_bits_to_values_host(qba_ctx *ctx, const int64_t *raw_host, uint64_t count, int nq,
+                                       uint8_t *vals, qba_stream stream) {
+  if (!ctx || nq < 1 || nq > 8 || (count && (!raw_host || !vals)))
+    return qba_fail(QBA_EINVAL, "qba_bits_to_values_host: bad arguments (1 <= nq <= 8)");
+  if (count == 0) return QBA_OK;
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  const size_t n = count * (size_t)nq;
+  if ((rc = qba_ensure_staging(ctx, 8 * n, 8 * n))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  memcpy(ctx->pin_h, raw_host, 8 * n);
+  QBA_HIP(hipMemcpyAsync(ctx->pin_d, ctx->pin_h, 8 * n, hipMemcpyHostToDevice, s));
+  const unsigned grid = (unsigned)std::min<uint64_t>((count + 255) / 256, 8192);
+  hipLaunchKernelGGL(qba_k_bits_to_values, dim3(grid), dim3(256), 0, s, static_cast<const int64_t *>(ctx->pin_d),
+                     count, nq, vals);
+  QBA_HIP(hipGetLastError());
+  QBA_HIP(hipStreamSynchronize(s));
   return QBA_OK;
 }
 

@@ -157,6 +157,11 @@ struct qba_ctx {
   int64_t *count1 = nullptr; // 1-word device counter
   int64_t *stats = nullptr;  // [2]: last counts launch: Q entries with a value >= w, spare
   uint64_t chunk = QBA_CHUNK;  // entries per list-kernel launch (env QBA_CHUNK_ENTRIES, tests)
+  // pinned host + device staging of the synchronous *_host entry points
+  void *pin_h = nullptr;
+  size_t pin_h_bytes = 0;
+  void *pin_d = nullptr;
+  size_t pin_d_bytes = 0;
   // RCCL communicator of the GPU-owner ranks (qba_rccl_init), or null
   void *rccl_comm = nullptr;
   int rccl_ranks = 0;
@@ -165,6 +170,7 @@ void qba_rccl_release(qba_ctx *ctx);
 
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes);
 int qba_ensure_scan(qba_ctx *ctx, size_t bytes);
+int qba_ensure_staging(qba_ctx *ctx, size_t host_bytes, size_t dev_bytes);
 int qba_set_device(qba_ctx *ctx);
 
 static inline int qba_nq(int n) {  // ceil(log2(n+1)), tfg.py:317

@@ -989,10 +989,24 @@ __global__ void __launch_bounds__(256)
 #define QBA_GRID_QPT 2
 #endif
 static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count) {
+  // the occupancy query costs tens of microseconds: cached per (kernel, LDS)
+  struct Occ {
+    const void *k;
+    size_t lds;
+    int per_cu;
+  };
+  static thread_local Occ cache[16] = {};
+  static thread_local int next = 0;
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, QBA_LBLOCK, lds) != hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
+  for (const Occ &o : cache)
+    if (o.k == kern && o.lds == lds) per_cu = o.per_cu;
+  if (per_cu == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, QBA_LBLOCK, lds) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    cache[next] = Occ{kern, lds, per_cu};
+    next = (next + 1) % 16;
+  }
   const uint64_t nquad = (count + 3) >> 2;
   // >= 2 quads (one wide thread-step) per thread: a small launch (configs[1],
   // 1e6 entries) spreads over 163 workgroups instead of 82

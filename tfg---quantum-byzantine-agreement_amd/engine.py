@@ -291,38 +291,21 @@ class Engine:
         call("qba_gather", self.ctx, _ptr(li), li.numel(), _ptr(d_idx), m, _ptr(out), self.stream())
         return out.cpu().numpy()
 
-    def _staging(self, n_stage: int, n_out: int):
-        """Reusable pinned host / device staging for check_packet (grown on demand)."""
-        if getattr(self, "_st_cap", (0, 0))[0] < n_stage or self._st_cap[1] < n_out:
-            cs, co = max(n_stage, 4096), max(n_out, 4096)
-            self._st_h = torch.empty(cs, dtype=torch.int64).pin_memory()
-            self._st_d = torch.empty(cs, dtype=torch.int64, device=self.device)
-            self._out_h = torch.empty(co, dtype=torch.int64).pin_memory()
-            self._out_d = torch.empty(co, dtype=torch.int64, device=self.device)
-            self._st_cap = (cs, co)
-        return self._st_h, self._st_d, self._out_h, self._out_d
-
     def check_packet(self, li: torch.Tensor, order: np.ndarray, rows: Sequence[Sequence[int]], v: int,
                      w: int) -> Tuple[tuple, bool]:
         """One packet of the exact-order protocol (tfg.py:189-192, 291-294):
         own = tuple(Li[j] for j in order) and Cond2/Cond3 of
-        consistent(v, rows | {own}, w), in one launch and one host sync.  All
-        rows must have len(order) entries (Cond1 stays with the caller)."""
+        consistent(v, rows | {own}, w), in one launch and one host sync
+        (qba_check_packet_host).  All rows must have len(order) entries
+        (Cond1 stays with the caller)."""
         ln, m = len(order), len(rows)
-        st_h, st_d, out_h, out_d = self._staging(ln * (m + 1), ln + 3 + m)
-        hv = st_h.numpy()
-        hv[:ln] = order
+        stage = np.empty(ln * (m + 1), np.int64)
+        stage[:ln] = order
         if m and ln:
-            hv[ln:ln * (m + 1)] = np.asarray(rows, dtype=np.int64).reshape(-1)
-        n_st, n_out = ln * (m + 1), ln + 3 + m
-        stream = torch.cuda.current_stream(self.device)
-        if n_st:
-            st_d[:n_st].copy_(st_h[:n_st], non_blocking=True)
-        call("qba_check_packet", self.ctx, _ptr(li), li.numel(), _ptr(st_d), m, ln, int(v), int(w),
-             _ptr(out_d), self.stream())
-        out_h[:n_out].copy_(out_d[:n_out], non_blocking=True)
-        stream.synchronize()
-        o = out_h[:n_out].numpy()
+            stage[ln:] = np.asarray(rows, dtype=np.int64).reshape(-1)
+        o = np.empty(ln + 3 + m, np.int64)
+        call("qba_check_packet_host", self.ctx, _ptr(li), li.numel(), stage.ctypes.data, m, ln, int(v), int(w),
+             o.ctypes.data, self.stream())
         if o[ln]:
             raise QbaError("qba_check_packet: index outside the list")
         eq = o[ln + 3:]
@@ -330,6 +313,20 @@ class Engine:
         if m and not ln:  # every tuple empty: the set is {()}, vacuously consistent
             ok = True
         return tuple(o[:ln].tolist()), ok
+
+    def lists_to_bits(self, lists: torch.Tensor, rows: int, count: int, nq: int) -> np.ndarray:
+        """rawS (tfg.py:81-84): rows [0, rows) encoded, host int64 [rows, count*nq]."""
+        out = np.empty((rows, count * nq), np.int64)
+        call("qba_lists_to_bits_host", self.ctx, _ptr(lists), lists.stride(0), rows, count, nq,
+             out.ctypes.data, self.stream())
+        return out
+
+    def bits_to_values_host(self, raw: np.ndarray, count: int, nq: int) -> torch.Tensor:
+        """measure_to_ints (tfg.py:158, 161) of a received host buffer -> device list."""
+        raw = np.ascontiguousarray(raw, dtype=np.int64)
+        out = torch.empty(max(count, 1), dtype=torch.uint8, device=self.device)
+        call("qba_bits_to_values_host", self.ctx, raw.ctypes.data, count, nq, _ptr(out), self.stream())
+        return out[:count]
 
     def allreduce_i64(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum over the RCCL communicator of rccl_init (qba_allreduce_i64)."""

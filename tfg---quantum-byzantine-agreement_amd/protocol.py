@@ -62,11 +62,10 @@ def generacionListas(nParties, size, nQubits, w, engine=None, seed=0, lists=None
         if arr.shape != (nParties + 1, size):
             raise ValueError(f"injected lists must have shape {(nParties + 1, size)}")
         dev = engine.to_device(arr)
-    rows = [engine.values_to_bits(dev[g, :size], size, nQubits) for g in range(nParties + 1)]
-    if hasattr(rows[0], "new_empty"):  # device tensors: one stack, one copy to the host
-        import torch
-        return engine.to_host(torch.stack(rows))
-    return np.stack([engine.to_host(r) for r in rows])
+    if hasattr(engine, "lists_to_bits"):  # every row encoded on the device, one copy to the host
+        return engine.lists_to_bits(dev, nParties + 1, size, nQubits)
+    return np.stack([engine.to_host(engine.values_to_bits(dev[g, :size], size, nQubits))
+                     for g in range(nParties + 1)])
 
 
 def measure_to_ints(raw, sizeL, nQubits, engine=None):
@@ -232,6 +231,8 @@ class Party:
         self.li = self._decode(mine)
 
     def _decode(self, raw):
+        if hasattr(self.engine, "bits_to_values_host"):  # straight from the receive buffer
+            return self.engine.bits_to_values_host(raw, self.sizeL, self.nq)
         return self.engine.bits_to_values(self.engine.to_device(raw), self.sizeL, self.nq)
 
     # tfg.py:327-330
