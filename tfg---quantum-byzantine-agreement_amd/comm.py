@@ -109,13 +109,16 @@ class Request:
         if self._post is None:
             return
         w = self._world
-        with w._cv:
-            ok = w._cv.wait_for(lambda: self._post.done or w._failed, timeout=w.timeout)
-            if w._failed:
-                raise RuntimeError("LocalWorld aborted by another rank")
-            if not ok:
-                w._fail()
-                raise TimeoutError("LocalWorld receive timed out (protocol deadlock?)")
+        if w.coop:
+            w._coop_wait(lambda: self._post.done)
+        else:
+            with w._cv:
+                ok = w._cv.wait_for(lambda: self._post.done or w._failed, timeout=w.timeout)
+                if w._failed:
+                    raise RuntimeError("LocalWorld aborted by another rank")
+                if not ok:
+                    w._fail()
+                    raise TimeoutError("LocalWorld receive timed out (protocol deadlock?)")
         if status is not None:
             status.source, status.tag = self._post.status.source, self._post.status.tag
 
@@ -155,20 +158,56 @@ class LocalComm:
 
     def Barrier(self) -> None:
         w = self.world
-        try:
-            w._barrier.wait(timeout=w.timeout)
-        except threading.BrokenBarrierError:
-            w._fail()
-            raise RuntimeError("LocalWorld barrier broken (a rank failed or timed out)")
+        if w.coop:
+            gen = w._bar_gen
+            w._bar_count += 1
+            if w._bar_count == w.size:
+                w._bar_count = 0
+                w._bar_gen += 1
+            else:
+                w._coop_wait(lambda: w._bar_gen != gen)
+        else:
+            try:
+                w._barrier.wait(timeout=w.timeout)
+            except threading.BrokenBarrierError:
+                w._fail()
+                raise RuntimeError("LocalWorld barrier broken (a rank failed or timed out)")
         self.epoch += 1
 
 
-class LocalWorld:
-    """An in-process MPI world of ``size`` ranks, one thread each."""
+def _greenlet():
+    try:
+        import greenlet  # type: ignore
+        return greenlet
+    except ImportError:
+        return None
 
-    def __init__(self, size: int, timeout: float = 120.0):
+
+class LocalWorld:
+    """An in-process MPI world of ``size`` ranks.
+
+    Two schedulers, same delivery semantics (so the same results):
+    * ``coop`` (default when the ``greenlet`` module is importable and
+      QBA_LOCAL_THREADS is unset): every rank is a greenlet of ONE thread and
+      a blocking call (an unmatched receive, a barrier) switches to the next
+      runnable rank -- no thread wake-ups and no GIL hand-offs around the
+      engine's device calls; a world where no rank can run is a deadlock
+      (RuntimeError);
+    * threads: one thread per rank (the rounds as concurrent processes),
+      with ``timeout`` on every blocking call.
+    """
+
+    def __init__(self, size: int, timeout: float = 120.0, coop: Optional[bool] = None):
         if size < 1:
             raise ValueError("world size must be >= 1")
+        import os
+        if coop is None:
+            coop = _greenlet() is not None and os.environ.get("QBA_LOCAL_THREADS") != "1"
+        self.coop = bool(coop)
+        self._waiting: List[Optional[Callable[[], bool]]] = [None] * size
+        self._bar_count = 0
+        self._bar_gen = 0
+        self._sched = None
         self.size = size
         self.timeout = timeout
         self._cv = threading.Condition()
@@ -231,6 +270,61 @@ class LocalWorld:
                 status.source, status.tag = best[1].src, best[1].tag
             return True
 
+    # -- cooperative scheduling (coop) ------------------------------------
+    def _coop_wait(self, ready: Callable[[], bool]) -> None:
+        """Block the calling rank's greenlet until ready() holds."""
+        if ready():
+            return
+        r = _tls.comm.rank
+        self._waiting[r] = ready
+        self._sched.switch()
+        if self._failed:
+            raise RuntimeError("LocalWorld aborted by another rank")
+
+    def _run_coop(self, fn) -> List[Any]:
+        glet = _greenlet()
+        results: List[Any] = [None] * self.size
+        errors: List[Optional[BaseException]] = [None] * self.size
+        self._sched = glet.getcurrent()
+
+        def body(r: int) -> None:
+            try:
+                results[r] = fn(self.comms[r])
+            except BaseException as exc:  # noqa: BLE001 - re-raised below
+                errors[r] = exc
+                self._failed = True
+
+        lets = [glet.greenlet(lambda r=r: body(r), parent=self._sched) for r in range(self.size)]
+        prev = getattr(_tls, "comm", None)
+        try:
+            while True:
+                live = [r for r in range(self.size) if not lets[r].dead]
+                if not live:
+                    break
+                ran = False
+                for r in live:
+                    w = self._waiting[r]
+                    if w is not None and not (self._failed or w()):
+                        continue
+                    self._waiting[r] = None
+                    _tls.comm = self.comms[r]
+                    lets[r].switch()
+                    ran = True
+                if not ran:
+                    self._failed = True
+                    for r in live:
+                        errors[r] = errors[r] or RuntimeError("LocalWorld deadlock: no rank can proceed")
+                    break
+        finally:
+            _tls.comm = prev
+        primary = [e for e in errors if e is not None and not _is_echo(e)]
+        if primary:
+            raise primary[0]
+        echoes = [e for e in errors if e is not None]
+        if echoes:
+            raise echoes[0]
+        return results
+
     # -- running ---------------------------------------------------------
     def run(self, fn: Callable[[LocalComm], Any]) -> List[Any]:
         """Run ``fn(comm)`` on every rank in its own thread; return per-rank results.
@@ -239,6 +333,8 @@ class LocalWorld:
         ranks are released) as-is, so protocol errors such as the reference's
         ``ValueError`` from ``min(set())`` surface unchanged.
         """
+        if self.coop:
+            return self._run_coop(fn)
         results: List[Any] = [None] * self.size
         errors: List[Optional[BaseException]] = [None] * self.size
 
