@@ -97,6 +97,13 @@ def cpu_baseline_counts(n, seed, info, target_s):
                       f"(oracle/sampler_ref.c) sample + count, {dt:.1f} s"}
 
 
+def _lib_sha16():
+    """sha256 (16 hex) of the libqba.so this process loads (PMC figures are per build)."""
+    import hashlib
+    lib = importlib.import_module(f"{PKG}._lib")
+    return hashlib.sha256(Path(lib.LIB_PATH).read_bytes()).hexdigest()[:16]
+
+
 # ---------------------------------------------------------------------------
 # configs[2]: the headline (default)
 # ---------------------------------------------------------------------------
@@ -164,12 +171,16 @@ def headline(args):
     value = entries / t_max
     bytes_per_entry = 2 * (n + 1)
     achieved = bytes_per_entry * per / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, traffic_note = None, "no PMC traffic file for this workload"
     tp = Path(args.traffic)
     if tp.exists():
         tj = json.loads(tp.read_text())
+        sha = _lib_sha16()
         if tj.get("per_launch_entries") == per and tj.get("n") == n and tj.get("mode") == args.mode:
-            traffic = tj.get("hbm_bytes_per_launch")
+            if tj.get("libqba_sha16") == sha:
+                traffic, traffic_note = tj.get("hbm_bytes_per_launch"), f"PMC FETCH+WRITE of this build ({sha})"
+            else:
+                traffic_note = f"stale: {tp.name} was measured on build {tj.get('libqba_sha16')}, running {sha}"
     out = {
         "metric": METRIC,
         "value": value,
@@ -203,6 +214,10 @@ def headline(args):
             # kernel never re-reads the lists, so this sits near half of frac
             "traffic_gbs": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
             "traffic_frac": traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
+            "traffic_source": traffic_note,
+            "note": "achieved/frac count the BASELINE's 24 B/entry (lists written + read back once); the fused "
+                    "kernel writes them once and never re-reads, so the bytes HBM really moves are "
+                    "traffic (traffic_gbs / traffic_frac)",
         },
         "verification": {"q_entries": int(Pn.sum()), "offdiag_collisions": offdiag},
     }

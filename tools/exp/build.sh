@@ -12,5 +12,6 @@ F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -fvisibility=hidden -munsafe-fp-at
 /opt/rocm/bin/hipcc $F -DQBA_ONLY_N=11 "$@" -c $src/qba_lists.hip -o $out/$name.o
 /opt/rocm/bin/hipcc $F -DQBA_INST_N=11 "$@" -c $src/qba_lists_inst.hip -o $out/${name}_n11.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/$name.so $out/$name.o $out/${name}_n11.o \
-  $here/../_build/qba_ctx.o $here/../_build/qba_exact.o $here/../_build/qba_sv.o $here/../_build/qba_resource.o
+  $here/../_build/qba_ctx.o $here/../_build/qba_exact.o $here/../_build/qba_sv.o $here/../_build/qba_resource.o \
+  $here/../_build/qba_rccl.o $here/../_build/qba_plan.o -ldl
 rm -f $out/$name.o $out/${name}_n11.o

@@ -11,7 +11,9 @@ row stores against the known list bytes written per launch ((n+1) B/entry).
     python tools/pmc_traffic.py <pmc dir> <entries per launch> <n> [mode]
 """
 import csv
+import hashlib
 import json
+import os
 import statistics
 import sys
 from pathlib import Path
@@ -30,5 +32,9 @@ out = {"n": n, "per_launch_entries": per, "mode": mode,
        "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
        "write_calibration": {"known_list_bytes": known, "write_over_known": write / known},
        "algorithmic_bytes_per_launch": 2 * (n + 1) * per,
-       "source": str(root), "kernel": f"qba_k_lists<{n},1,*>"}
+       "source": str(root), "kernel": f"qba_k_lists<{n},1,*>",
+       # the library the counters were read from: bench.py drops the figure for any other build
+       "libqba_sha16": hashlib.sha256(open(os.environ.get("QBA_LIB", Path(__file__).resolve().parent.parent
+                                                         / "tfg---quantum-byzantine-agreement_amd" / "_build"
+                                                         / "libqba.so"), "rb").read()).hexdigest()[:16]}
 print(json.dumps(out, indent=1))
