@@ -809,8 +809,13 @@ __device__ __forceinline__ void qba_zero_outputs(const QbaZero &z, int tid, int 
   if ((z.flags & 2) && z.stats && tid < C::STATS) z.stats[tid] = 0;
 }
 
+#ifdef QBA_MINW  // experiment builds: minimum waves per SIMD (caps the VGPRs)
+#define QBA_LISTS_BOUNDS __launch_bounds__(QBA_LBLOCK, QBA_MINW)
+#else
+#define QBA_LISTS_BOUNDS __launch_bounds__(QBA_LBLOCK)
+#endif
 template <int NP, int MODE, int SAMP, int QPT>
-__global__ void __launch_bounds__(QBA_LBLOCK)
+__global__ void QBA_LISTS_BOUNDS
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                 uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
                 uint32_t *__restrict__ slab, QbaZero zero) {
