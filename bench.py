@@ -361,6 +361,8 @@ def config4(args, eng):
     gates = np.array([(0, 0, -1)] + [(1, t, 0) for t in range(1, q)], np.int32)  # GHZ register
     eng.statevector(q, gates[:1], out=sv)
     torch.cuda.synchronize()
+    idx0, _ = eng.support(sv, q, cap=16)  # the register after H: |0...0> + |10...0>
+    assert list(idx0) == [0, 1 << (q - 1)], idx0
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     eng.apply_gates(sv, q, gates[1:])
@@ -373,6 +375,11 @@ def config4(args, eng):
     b2.record()
     torch.cuda.synchronize()
     prep = a2.elapsed_time(b2) * 1e-3
+    a2.record()
+    eng.statevector_unfused(q, gates, out=sv)  # init pass + H pass + CX pass
+    b2.record()
+    torch.cuda.synchronize()
+    prep_unfused = a2.elapsed_time(b2) * 1e-3
     idx, prob = eng.support(sv, q, cap=16)
     # the fused CX pass reads and writes the control = 1 half once: 8 B per amplitude of the state
     gbs = 8 * (1 << q) / t / 1e9
@@ -389,7 +396,10 @@ def config4(args, eng):
                   "note": f"the {q - 1} CX gates share their control: one XOR-mask pass over the "
                           "control = 1 half (read + written once)"},
                  {"ms_per_step": t * 1e3,
-                  "register_prep_ms": prep * 1e3, "cx_gates_fused_per_pass": q - 1,
+                  "register_prep_ms": prep * 1e3, "register_prep_unfused_ms": prep_unfused * 1e3,
+                  "register_prep_note": "prep = qba_sv_prepare: H folded into the init pass (write-only), "
+                                        "then the CX pass; unfused = init pass + H pass + CX pass",
+                  "cx_gates_fused_per_pass": q - 1,
                   "verification": {"support": [int(i) for i in idx], "probs": [float(p) for p in prob],
                                    "ghz_exact": bool(ok)},
                   "full_circuit_n7": full}, dtype="f64")

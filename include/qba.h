@@ -76,6 +76,13 @@ QBA_API int qba_reserve(qba_ctx *ctx, int n_parties, int64_t max_blocks);
 QBA_API int qba_sv_init(qba_ctx *ctx, double *sv_dev, int nqubits, qba_stream stream);
 QBA_API int qba_sv_apply(qba_ctx *ctx, double *sv_dev, int nqubits, const int32_t *gates_host,
                  int n_gates, qba_stream stream);
+/* |0...0> followed by the gate list, in the fewest passes: single-qubit gates
+ * on qubits no CX has touched yet fold into the initial product state (one
+ * write-only pass), then runs of H / X / shared-control CX gates are one pass
+ * each.  Same result as qba_sv_init + qba_sv_apply (tfg.py:56-65, 43-52:
+ * the whole H/X layer of both circuits folds into the init pass). */
+QBA_API int qba_sv_prepare(qba_ctx *ctx, double *sv_dev, int nqubits, const int32_t *gates_host,
+                   int n_gates, qba_stream stream);
 /* Probabilities |a_i|^2 > eps, compacted in ascending index order.  Writes at
  * most `cap` (index, prob) pairs; *count_host receives the full support size.
  * Synchronous. */

@@ -264,6 +264,73 @@ def test_statevector_random_circuits_fused_runs(engine, q):
         assert np.max(np.abs(sv.cpu().numpy() - ref)) < 1e-12, (q, trial)
 
 
+@pytest.mark.parametrize("q", [1, 2, 4, 7, 12])
+def test_statevector_fused_h_and_product_prefix(engine, q):
+    """Gate fusion of qba_sv_prepare / qba_sv_apply vs the dense oracle, which
+    applies every gate on its own: random single-qubit layers (H, X, repeated
+    H that cancel, H X H = Z-type sign flips) folded into the init pass,
+    interleaved with CX gates after which single-qubit gates on touched
+    qubits must stay in order, and long H runs over > QBA_HSET_MAX qubits
+    (several Walsh-Hadamard passes, bit 0 in and out of the set)."""
+    rng = np.random.default_rng(7000 + q)
+    for trial in range(8):
+        ops = []
+        for _ in range(int(rng.integers(4, 30))):  # single-qubit prefix layer
+            ops.append((["H", "X"][int(rng.integers(2))], int(rng.integers(q)), -1))
+        while len(ops) < 60:
+            r = rng.integers(4)
+            if r == 0 and q > 1:
+                c = int(rng.integers(q))
+                t = int(rng.integers(q - 1))
+                ops.append(("X", t + (t >= c), c))
+            elif r == 1:  # an H run over a random subset, possibly repeated qubits
+                for t in rng.integers(q, size=int(rng.integers(1, 2 * q + 1))):
+                    ops.append(("H", int(t), -1))
+            else:
+                ops.append((["H", "X"][int(rng.integers(2))], int(rng.integers(q)), -1))
+        trip = np.array([(0 if g == "H" else 1, t, c) for g, t, c in ops], np.int32)
+        ref = sv_oracle.run(ops, q)
+        for fn in (engine.statevector, engine.statevector_unfused):
+            sv = fn(q, trip)
+            torch.cuda.synchronize()
+            assert np.max(np.abs(sv.cpu().numpy() - ref)) < 1e-12, (q, trial, fn.__name__)
+    # all-H register: one product pass, uniform amplitudes
+    trip = np.array([(0, t, -1) for t in range(q)], np.int32)
+    sv = engine.statevector(q, trip).cpu().numpy()
+    assert np.max(np.abs(sv - 2.0 ** (-q / 2))) < 1e-15
+
+
+@pytest.mark.parametrize("q", [2, 3, 6, 11])
+def test_statevector_commuting_cx_windows(engine, q):
+    """Windows of pairwise-commuting X / CX gates with several controls (one
+    qba_k_sv_xmulti pass, controls on bit 0 -> scalar path, > 8 controls ->
+    window split), broken by a gate whose target is a window control -- vs
+    the dense oracle."""
+    rng = np.random.default_rng(9100 + q)
+    for trial in range(10):
+        ops = [(["H", "X"][int(rng.integers(2))], int(rng.integers(q)), -1) for _ in range(2 * q)]
+        for _ in range(4):
+            perm = rng.permutation(q)
+            nc = int(rng.integers(1, max(2, q // 2) + 1))
+            ctl, tgt = [int(x) for x in perm[:nc]], [int(x) for x in perm[nc:]]
+            if not tgt:
+                continue
+            for _ in range(int(rng.integers(1, 3 * q))):
+                t = tgt[int(rng.integers(len(tgt)))]
+                c = -1 if rng.random() < 0.2 else ctl[int(rng.integers(len(ctl)))]
+                ops.append(("X", t, c))
+            if rng.random() < 0.5:  # breaks the window: a control becomes a target
+                ops.append(("X", ctl[0], tgt[0]))
+            if rng.random() < 0.3:
+                ops.append(("H", int(rng.integers(q)), -1))
+        trip = np.array([(0 if g == "H" else 1, t, c) for g, t, c in ops], np.int32)
+        ref = sv_oracle.run(ops, q)
+        for fn in (engine.statevector, engine.statevector_unfused):
+            sv = fn(q, trip)
+            torch.cuda.synchronize()
+            assert np.max(np.abs(sv.cpu().numpy() - ref)) < 1e-12, (q, trial, fn.__name__)
+
+
 def test_ghz_register_statevector(engine):
     """One entangled register of the Q resource (n+1 qubits) at n=19: support
     {0...0, 1...1}, each 1/2 (the per-register closed form of A2)."""

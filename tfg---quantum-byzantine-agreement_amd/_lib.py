@@ -33,6 +33,7 @@ SIGNATURES = {
     "qba_reserve": [_p, C.c_int, _i64],
     "qba_sv_init": [_p, _p, C.c_int, _p],
     "qba_sv_apply": [_p, _p, C.c_int, _pi32, C.c_int, _p],
+    "qba_sv_prepare": [_p, _p, C.c_int, _pi32, C.c_int, _p],
     "qba_sv_support": [_p, _p, C.c_int, _f64, _p, _p, _i64, _pi64, _p],
     "qba_resource_compile": [_p, C.c_int, C.c_int, _pi32, C.c_int, _pi32],
     "qba_program_export": [_p, C.c_int, C.c_int, _pi32, _pi32, _pu64, _pu64, _pu64, _i32, _pi32],

@@ -392,6 +392,11 @@ __device__ __forceinline__ void qba_t4(uint32_t a, uint32_t b, uint32_t c, uint3
   r3 = qba_perm_b(t3, t1, 0x07060302u);
 }
 
+// Inline asm in this file (here and qba_add_byte below) reads and writes
+// VGPRs only: no SGPR operand is written by VALU inside an asm block, so the
+// VALU-writes-SGPR -> VMEM-reads-SGPR hazard the compiler cannot see through
+// asm (the cause of the faulting saddr-store experiment)
+// does not arise.  Keep any new asm VGPR-only.
 // v_pk_lshlrev_b16: each 16-bit half of `one` shifted by the low 4 bits of
 // the same half of `amt` (the upper bits of the half are ignored by the ALU).
 __device__ __forceinline__ uint32_t qba_pk_onehot(uint32_t amt, uint32_t one) {

@@ -48,8 +48,7 @@ static int simulate_register(qba_ctx *ctx, const std::vector<int> &qubits,
   } guard{sv};
   int rc;
   if (q == 0) return qba_fail(QBA_EINVAL, "empty register");
-  if ((rc = qba_sv_init(ctx, sv, q, nullptr))) return rc;
-  if ((rc = qba_sv_apply(ctx, sv, q, g.data(), (int)g.size() / 3, nullptr))) return rc;
+  if ((rc = qba_sv_prepare(ctx, sv, q, g.data(), (int)g.size() / 3, nullptr))) return rc;
   const int64_t cap = 1 << 16;
   int64_t *idx_d = nullptr;
   double *prob_d = nullptr;

@@ -370,6 +370,15 @@ class Engine:
                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
         sv = out if out is not None else torch.empty(1 << nqubits, dtype=torch.float64, device=self.device)
         g = np.ascontiguousarray(gates, dtype=np.int32).reshape(-1, 3)
+        call("qba_sv_prepare", self.ctx, _ptr(sv), nqubits, _i32p(g), len(g), self.stream())
+        return sv
+
+    def statevector_unfused(self, nqubits: int, gates: np.ndarray,
+                            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """qba_sv_init + qba_sv_apply: no folding of the single-qubit layer into
+        the init pass (the H/X/CX run fusion of qba_sv_apply still applies)."""
+        sv = out if out is not None else torch.empty(1 << nqubits, dtype=torch.float64, device=self.device)
+        g = np.ascontiguousarray(gates, dtype=np.int32).reshape(-1, 3)
         call("qba_sv_init", self.ctx, _ptr(sv), nqubits, self.stream())
         call("qba_sv_apply", self.ctx, _ptr(sv), nqubits, _i32p(g), len(g), self.stream())
         return sv
