@@ -491,6 +491,40 @@ def test_chunked_launches(monkeypatch):
         eng.close()
 
 
+def test_counts_repeated_accumulate_stats():
+    """The count reduction (slab rows + qba_k_reduce) against the oracle on a
+    fresh context: several n, repeated launches, accumulation, check-only
+    launches and the stats of out-of-range values (set, then cleared)."""
+    eng = sub("engine").Engine(0)
+    try:
+        for n, count in [(1, 999), (3, 10_001), (11, 123_457), (11, 5), (15, 4099)]:
+            info = eng.prepare(n)
+            seed = 4242 + n
+            ref = oracle_lib.sample(n, seed, 7, count, info["notq"], info["q"], info["closed"])
+            H, C, P, bad = oracle_lib.counts(ref, n)
+            for _ in range(3):
+                lists, c = eng.sample_check(n, seed, 7, count)
+                gH, gC, gP = c.numpy()
+                assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P), (n, count)
+            eng.sample_check(n, seed, 7, count, lists, c, accumulate=True)
+            gH, gC, gP = c.numpy()
+            assert np.array_equal(gH, 2 * H) and np.array_equal(gC, 2 * C) and np.array_equal(gP, 2 * P)
+            c2 = eng.check_counts(lists, n, count)
+            assert np.array_equal(c2.numpy()[0], H)
+        n, count = 7, 10_000
+        eng.prepare(n)
+        lists = eng.sample(n, 5, 0, count)
+        bad = lists.clone()
+        q = (bad[0, :count] != bad[1, :count]).nonzero()[:3, 0]
+        bad[5, q] = 200
+        eng.check_counts(bad, n, count)
+        assert eng.last_stats()[0] == 3
+        eng.check_counts(lists, n, count)
+        assert eng.last_stats()[0] == 0
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("count", [1, 3, 4, 5, 7, 8, 9, 15, 17, 4099])
 def test_tiny_and_ragged_counts(engine, count):
     """Tail handling: fewer entries than one thread-step, ragged remainders

@@ -49,8 +49,8 @@ extern "C" int qba_init(int device, qba_ctx **out) {
   }
   if (hipMalloc(&ctx->flag, 64) != hipSuccess || hipMalloc(&ctx->count1, 64) != hipSuccess ||
       hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess) {
-    delete ctx;
-    return qba_fail(QBA_ENOMEM, "qba_init: hipMalloc of flags failed");
+    qba_destroy(ctx);
+    return qba_fail(QBA_ENOMEM, "qba_init: device scratch allocation failed");
   }
   *out = ctx;
   return QBA_OK;

@@ -829,6 +829,10 @@ __global__ void QBA_LISTS_BOUNDS
   extern __shared__ __align__(16) uint64_t lds[];
   const uint64_t *pat, *apat, *thr;
   const uint32_t *pl;
+#ifdef QBA_EXP_TIMING  // experiment builds: per-workgroup phase timestamps after the slab rows
+  uint64_t *tsl = reinterpret_cast<uint64_t *>(slab + (size_t)gridDim.x * C::NBP) + 4 * blockIdx.x;
+  const uint64_t ts0 = wall_clock64();
+#endif
   uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
   if (MODE != 0) {
     for (int i = threadIdx.x; i < C::NBP; i += BS) hist[i] = 0u;
@@ -837,7 +841,13 @@ __global__ void QBA_LISTS_BOUNDS
 #endif
   }
   __syncthreads();
-  const uint32_t nunits = count / (4 * QPT);
+#ifdef QBA_EXP_TIMING
+  const uint64_t ts1 = wall_clock64();
+#endif
+#ifndef QBA_EXP_SKIP  // experiment builds only: 1 = no main loop / tail, 2 = no slab flush
+#define QBA_EXP_SKIP 0
+#endif
+  const uint32_t nunits = (QBA_EXP_SKIP & 1) ? 0u : count / (4 * QPT);
   // the grid stride in an SGPR, read once: reloading gridDim in the loop is a
   // scalar load whose s_waitcnt lgkmcnt(0) also drains every LDS atomic the
   // wave has in flight (-2% step time)
@@ -862,7 +872,7 @@ __global__ void QBA_LISTS_BOUNDS
   }
   // the remaining < 4 QPT entries: whole quads, then the partial one
   const uint32_t r0 = nunits * (4 * QPT), rq = (count - r0 + 3) >> 2;
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x < rq) {
+  if (!(QBA_EXP_SKIP & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x < rq) {
     const uint32_t c0 = r0 + 4 * threadIdx.x;
     if (c0 + 4 <= count)
       qba_step<NP, MODE, SAMP, 1, false>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
@@ -871,9 +881,21 @@ __global__ void QBA_LISTS_BOUNDS
   }
   if (MODE != 0) {
     __syncthreads();
+#ifdef QBA_EXP_TIMING
+    const uint64_t ts2 = wall_clock64();
+#endif
     uint4 *dst = reinterpret_cast<uint4 *>(slab + (size_t)blockIdx.x * C::NBP);
     const uint4 *src = reinterpret_cast<const uint4 *>(hist);
-    for (int i = threadIdx.x; i < C::NBP / 4; i += BS) dst[i] = src[i];
+    if (!(QBA_EXP_SKIP & 2))
+      for (int i = threadIdx.x; i < C::NBP / 4; i += BS) dst[i] = src[i];
+#ifdef QBA_EXP_TIMING
+    if (threadIdx.x == 0) {
+      tsl[0] = ts0;
+      tsl[1] = ts1;
+      tsl[2] = ts2;
+      tsl[3] = wall_clock64();
+    }
+#endif
 #if QBA_ZERO_AT_END
     // any point of this kernel precedes the reduction; at the end it leaves
     // the main loop's code placement alone
