@@ -45,9 +45,24 @@ def _worker(rank, world, port, lists, n, out_q):
     first, cnt = d.shard_bounds(lists.shape[1], rank, world)
     H, C, P = orc.counts(lists[:, first:first + cnt], n)
     flat = torch.from_numpy(np.concatenate([H.ravel(), C.ravel(), P.ravel()]).copy())
+    base = flat.clone()
     d.allreduce_counts(flat)
     Hs, Cs, Ps = d.split_counts(flat, n)
-    out_q.put((rank, Hs.numpy().copy(), Cs.numpy().copy(), Ps.numpy().copy()))
+    # bench.py's N > 1 loop: asynchronous reductions into two alternating
+    # buffers, a buffer rewritten only after its reduction was waited for
+    bufs, pending, done = [torch.zeros_like(base), torch.zeros_like(base)], [None, None], []
+    for step in range(5):
+        b = step % 2
+        if pending[b] is not None:
+            pending[b].wait()
+            done.append(bufs[b].clone())
+        bufs[b].copy_(base * (step + 1))
+        pending[b] = d.allreduce_counts_async(bufs[b])
+    for b in (1, 0):  # steps 3, 4
+        pending[b].wait()
+        done.append(bufs[b].clone())
+    out_q.put((rank, Hs.numpy().copy(), Cs.numpy().copy(), Ps.numpy().copy(),
+               [x.numpy().copy() for x in done]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -69,8 +84,12 @@ def test_sharded_counts_allreduce_gloo(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     H, C, P = orc.counts(lists, n)
-    for _, Hs, Cs, Ps in res:
+    whole = np.concatenate([H.ravel(), C.ravel(), P.ravel()])
+    for _, Hs, Cs, Ps, steps in res:
         assert np.array_equal(Hs, H) and np.array_equal(Cs, C) and np.array_equal(Ps, P)
+        assert len(steps) == 5
+        for k, got in enumerate(steps):
+            assert np.array_equal(got, whole * (k + 1)), k
 
 
 def _countparty_worker(rank, world, port, spec, out_q):

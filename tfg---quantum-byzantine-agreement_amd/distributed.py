@@ -53,6 +53,15 @@ def allreduce_counts(flat: torch.Tensor) -> torch.Tensor:
     return flat
 
 
+def allreduce_counts_async(flat: torch.Tensor):
+    """Start the sum of the flat [H | C | P] buffer over ranks; returns the
+    work handle (wait() orders the caller's stream after it) or None when
+    there is nothing to reduce (one rank)."""
+    if torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1:
+        return torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, async_op=True)
+    return None
+
+
 def count_layout(n: int) -> Tuple[int, int, int, int]:
     """Sizes (H, C, P, total) of the flat count buffer for n parties."""
     w = 1 << int(n).bit_length()
