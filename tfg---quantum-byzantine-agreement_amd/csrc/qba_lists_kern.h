@@ -830,7 +830,7 @@ __global__ void QBA_LISTS_BOUNDS
   const uint64_t *pat, *apat, *thr;
   const uint32_t *pl;
 #ifdef QBA_EXP_TIMING  // experiment builds: per-workgroup phase timestamps after the slab rows
-  uint64_t *tsl = reinterpret_cast<uint64_t *>(slab + (size_t)gridDim.x * C::NBP) + 4 * blockIdx.x;
+  uint64_t *tsl = reinterpret_cast<uint64_t *>(slab + (size_t)gridDim.x * C::NBP) + 8 * blockIdx.x;
   const uint64_t ts0 = wall_clock64();
 #endif
   uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
@@ -894,6 +894,8 @@ __global__ void QBA_LISTS_BOUNDS
       tsl[1] = ts1;
       tsl[2] = ts2;
       tsl[3] = wall_clock64();
+      tsl[4] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));   // HW_ID: CU / SH / SE
+      tsl[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((32 - 1) << 11));  // XCC_ID
     }
 #endif
 #if QBA_ZERO_AT_END

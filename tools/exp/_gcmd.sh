@@ -1,5 +1,3 @@
 set -eo pipefail
-out=gpurun_out/w2; mkdir -p $out
-timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $out/b1.json 2> $out/b1.err
-bash tools/rehearse_world2.sh
-cp gpurun_out/world2/bench.json $out/world2.json; cp gpurun_out/world2/bench.err $out/world2.err
+out=gpurun_out/c1t; mkdir -p $out
+QBA_LIB=$PWD/tfg---quantum-byzantine-agreement_amd/_build/exp/t_timing.so timeout -k 10 200 python tools/exp/c1_timing.py > $out/timing2.txt 2>&1

@@ -14,7 +14,7 @@ root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, root)
 eng_mod = importlib.import_module("tfg---quantum-byzantine-agreement_amd.engine")
 n = 11
-for N in (1_000_000, 4_000_000):
+for N in (1_000_000, 2_000_000, 4_000_000):
     E = eng_mod.Engine(0)
     E.prepare(n)
     lists, counts = E.alloc_lists(n, N), E.alloc_counts(n)
@@ -28,10 +28,12 @@ for N in (1_000_000, 4_000_000):
     torch.cuda.synchronize()
     grid = min(-(-(N // 4) // (2 * 768)), 512)
     lib = ctypes.CDLL(os.environ["QBA_LIB"])
-    buf = np.zeros(grid * 4, np.uint64)
+    buf = np.zeros(grid * 8, np.uint64)
     rc = lib.qba_exp_timing(E.ctx, n, grid, buf.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0
-    t = buf.reshape(grid, 4).astype(np.int64)
+    t = buf.reshape(grid, 8)[:, :4].astype(np.int64)
+    hw = buf.reshape(grid, 8)[:, 4].astype(np.int64)
+    xcc = buf.reshape(grid, 8)[:, 5].astype(np.int64)
     t0 = t[:, 0].min()
     us = (t - t0) / 100.0
     def pct(x):
@@ -42,4 +44,9 @@ for N in (1_000_000, 4_000_000):
     print("  main+drain   ", pct(us[:, 2] - us[:, 1]))
     print("  flush(issue) ", pct(us[:, 3] - us[:, 2]))
     print("  last end     ", "%6.2f" % us[:, 3].max())
+    import collections
+    cu = collections.Counter(zip(xcc & 0xF, (hw >> 13) & 7, (hw >> 12) & 1, (hw >> 8) & 0xF))
+    per = collections.Counter(cu.values())
+    print("  workgroups per CU:", dict(sorted(per.items())), " distinct CUs:", len(cu),
+          " per XCC:", dict(sorted(collections.Counter(xcc & 0xF).items())))
     E.close()
