@@ -181,6 +181,17 @@ QBA_API int qba_check_packet(qba_ctx *ctx, const uint8_t *li_dev, uint64_t list_
                              const int64_t *stage_dev, int64_t m, int64_t len, int64_t v, int64_t w,
                              int64_t *out_dev, qba_stream stream);
 
+/* Exact-order consistent(v, L, w) (tfg.py:87-98) over m tuples gathered on
+ * the device (SURVEY.md §8(b) qba_check_gather): T_a[k] = lists[party[a]][
+ * idx[a][k]] (lists [rows][ld], list_len valid entries per row; idx [m][len]
+ * row-major).  L is a set: identical tuples collapse (tfg.py:209, 240, 260).
+ * *ok_dev = 1 consistent, 0 not, -1 an index or party out of range (nothing
+ * outside the lists is read).  1 <= m <= 64 (m = 0 is the reference's
+ * StopIteration, tfg.py:90: QBA_EINVAL).  Asynchronous on `stream`. */
+QBA_API int qba_check_gather(qba_ctx *ctx, const uint8_t *lists_dev, uint64_t ld, int rows, uint64_t list_len,
+                             const int64_t *idx_dev, const int32_t *party_dev, int64_t m, int64_t len,
+                             int64_t v, int64_t w, int32_t *ok_dev, qba_stream stream);
+
 /* Synchronous host-pointer form of qba_check_packet (the protocol's
  * per-packet call: one H2D through the context's pinned staging, one launch,
  * one D2H, one sync).  stage_host / out_host as above, in host memory. */

@@ -582,3 +582,46 @@ def test_adversarial_collisions_wide_and_narrow(engine):
         c = engine.check_counts(view, n, count)
         gH, gC, gP = c.numpy()
         assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P), off
+
+
+def test_check_gather_vs_oracle(engine):
+    """qba_check_gather: consistent(v, L, w) over tuples gathered
+    on the device from several parties' lists, each in its own index order --
+    against the oracle's consistent on the same tuples (as a set): honest
+    packets, duplicates that collapse, partial collisions, values > w and == v,
+    empty tuples, and out-of-range indices / parties."""
+    rng = np.random.default_rng(77)
+    n, count = 7, 5000
+    engine.prepare(n)
+    lists = engine.sample(n, 123, 0, count)
+    L = lists[:, :count].cpu().numpy().astype(np.int64)
+    w = 8
+    isq = np.nonzero(L[0] != L[1])[0]
+    checked = 0
+    for trial in range(60):
+        m = int(rng.integers(1, 6))
+        ln = int(rng.integers(0, 40))
+        base = rng.choice(isq, ln, replace=False) if ln else np.zeros(0, np.int64)
+        party = [int(x) for x in rng.choice(np.arange(2, n + 1), m)]
+        idx = np.stack([rng.permutation(base) if rng.random() < 0.5 else base for _ in range(m)]) \
+            if ln else np.zeros((m, 0), np.int64)
+        if trial % 7 == 3 and m > 1:
+            party[1] = party[0]
+            idx[1] = idx[0]  # identical tuple: collapses in the set
+        v = int(rng.integers(0, w + 2))
+        lv = L.copy()
+        if trial % 5 == 4 and ln:
+            lv[party[0], idx[0][0]] = w + 3  # value outside [0, w]
+        d = torch.zeros_like(lists)
+        d[:, :count] = torch.from_numpy(lv.astype(np.uint8))
+        tuples = {tuple(int(lv[party[a]][j]) for j in idx[a]) for a in range(m)}
+        want = orc.consistent(v, tuples, w)
+        assert engine.check_gather(d, count, idx, party, v, w) == want, trial
+        checked += 1
+    assert checked == 60
+    with pytest.raises(sub("engine").QbaError):
+        engine.check_gather(lists, count, np.array([[0, count]]), [2], 0, w)
+    with pytest.raises(sub("engine").QbaError):
+        engine.check_gather(lists, count, np.array([[0, 1]]), [n + 5], 0, w)
+    with pytest.raises(sub("engine").QbaError):
+        engine.check_gather(lists, count, np.zeros((0, 3), np.int64), [], 0, w)

@@ -219,6 +219,92 @@ extern "C" int qba_check_packet(qba_ctx *ctx, const uint8_t *li, uint64_t list_l
   return QBA_OK;
 }
 
+// --- consistent(v, L, w) over tuples gathered from the device lists (SURVEY.md
+// §8(b) qba_check_gather) ---------------------------------------------------------
+// T_a[k] = lists[party[a]][idx[a][k]] for m index orders of length len (each
+// tuple in its own order, as each lieutenant ships its own set-iteration
+// order, tfg.py:189, 291).  L is a set (tfg.py:209, 240, 260), so identical
+// tuples collapse: the pair (a, b) violates Cond3 iff 0 < eq(a, b) < len,
+// eq = the number of positions where T_a and T_b agree.  cnt (scratch):
+// [0] bad index/party, [1] Cond2 violation, [2 + pair] eq per pair a < b,
+// each workgroup adding its LDS partial once.
+#define QBA_GATHER_MAXM 64
+__global__ void __launch_bounds__(256)
+    qba_k_check_gather(const uint8_t *__restrict__ lists, uint64_t ld, int rows, uint64_t list_len,
+                       const int64_t *__restrict__ idx, const int32_t *__restrict__ party, int64_t m,
+                       int64_t len, int64_t v, int64_t w, unsigned long long *__restrict__ cnt) {
+  __shared__ unsigned int eq[QBA_GATHER_MAXM * (QBA_GATHER_MAXM - 1) / 2];
+  __shared__ unsigned int flags[2];
+  const int np = (int)(m * (m - 1) / 2);
+  for (int i = threadIdx.x; i < np; i += blockDim.x) eq[i] = 0u;
+  if (threadIdx.x < 2) flags[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < len;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    // values re-read per pair (m is small; a runtime-indexed private array
+    // would live in scratch)
+    auto val = [&](int64_t a) -> int64_t {
+      const int64_t j = idx[a * len + k];
+      const int32_t r = party[a];
+      if (r < 0 || r >= rows || (uint64_t)j >= list_len) return -1;
+      return lists[(uint64_t)r * ld + (uint64_t)j];
+    };
+    int p = 0;
+    for (int64_t a = 0; a < m; ++a) {
+      const int64_t xa = val(a);
+      if (xa < 0) atomicOr(&flags[0], 1u);
+      if (xa < 0 || xa > w || xa == v) atomicOr(&flags[1], 1u);
+      for (int64_t b = a + 1; b < m; ++b, ++p)
+        if (xa == val(b)) atomicAdd(&eq[p], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < np; i += blockDim.x)
+    if (eq[i]) atomicAdd(&cnt[2 + i], (unsigned long long)eq[i]);
+  if (threadIdx.x < 2 && flags[threadIdx.x]) atomicOr(&cnt[threadIdx.x], 1ull);
+}
+
+__global__ void qba_k_check_gather_fin(const unsigned long long *__restrict__ cnt, int64_t m, int64_t len,
+                                       int32_t *__restrict__ ok) {
+  if (threadIdx.x != 0) return;
+  int32_t r = 1;
+  if (cnt[0]) {
+    r = -1;
+  } else if (cnt[1]) {
+    r = 0;
+  } else {
+    const int64_t np = m * (m - 1) / 2;
+    for (int64_t p = 0; p < np; ++p)
+      if (cnt[2 + p] != 0ull && cnt[2 + p] != (unsigned long long)len) r = 0;
+  }
+  *ok = r;
+}
+
+extern "C" int qba_check_gather(qba_ctx *ctx, const uint8_t *lists, uint64_t ld, int rows, uint64_t list_len,
+                                const int64_t *idx, const int32_t *party, int64_t m, int64_t len, int64_t v,
+                                int64_t w, int32_t *ok, qba_stream stream) {
+  if (!ctx || !ok || m < 1 || m > QBA_GATHER_MAXM || len < 0 || rows < 1 || ld < list_len ||
+      (len && (!lists || !idx || !party)))
+    return qba_fail(QBA_EINVAL, "qba_check_gather: bad arguments (1 <= m <= 64 tuples required; "
+                                "an empty L is the reference's StopIteration, tfg.py:90)");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  const size_t ncnt = 2 + (size_t)(m * (m - 1) / 2);
+  if ((rc = qba_ensure_scan(ctx, ncnt * sizeof(unsigned long long)))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long *cnt = static_cast<unsigned long long *>(ctx->scan);
+  QBA_HIP(hipMemsetAsync(cnt, 0, ncnt * sizeof(unsigned long long), s));
+  if (len > 0) {
+    const unsigned grid = (unsigned)std::min<int64_t>((len + 255) / 256, 1024);
+    hipLaunchKernelGGL(qba_k_check_gather, dim3(grid), dim3(256), 0, s, lists, ld, rows, list_len, idx, party, m,
+                       len, v, w, cnt);
+    QBA_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(qba_k_check_gather_fin, dim3(1), dim3(64), 0, s, cnt, m, len, ok);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}
+
 // Synchronous host-pointer form (the protocol host's per-packet call): the
 // stage goes through the ctx's pinned staging, the result comes back to
 // out_host; one H2D, one launch, one D2H, one stream sync.

@@ -314,6 +314,24 @@ class Engine:
             ok = True
         return tuple(o[:ln].tolist()), ok
 
+    def check_gather(self, lists: torch.Tensor, count: int, idx: np.ndarray, party: Sequence[int], v: int,
+                     w: int) -> bool:
+        """consistent(v, L, w) (tfg.py:87-98) over the tuples
+        L = {tuple(lists[party[a]][j] for j in idx[a])}, gathered and checked on
+        the device (qba_check_gather; identical tuples collapse as in the
+        reference's set).  idx: int64 [m, len]."""
+        idx_d = torch.as_tensor(np.ascontiguousarray(idx, dtype=np.int64), device=self.device)
+        m = idx_d.shape[0]
+        ln = idx_d.shape[1] if idx_d.dim() == 2 else 0
+        party_d = torch.as_tensor(np.asarray(party, dtype=np.int32), device=self.device)
+        ok = torch.empty(1, dtype=torch.int32, device=self.device)
+        call("qba_check_gather", self.ctx, _ptr(lists), lists.stride(0), lists.shape[0], count, _ptr(idx_d),
+             _ptr(party_d), m, ln, int(v), int(w), _ptr(ok), self.stream())
+        r = int(ok.item())
+        if r < 0:
+            raise QbaError("qba_check_gather: index or party outside the lists")
+        return bool(r)
+
     def lists_to_bits(self, lists: torch.Tensor, rows: int, count: int, nq: int) -> np.ndarray:
         """rawS (tfg.py:81-84): rows [0, rows) encoded, host int64 [rows, count*nq]."""
         out = np.empty((rows, count * nq), np.int64)

@@ -1,3 +1,3 @@
 set -eo pipefail
-out=gpurun_out/c1t; mkdir -p $out
-QBA_LIB=$PWD/tfg---quantum-byzantine-agreement_amd/_build/exp/t_timing.so timeout -k 10 200 python tools/exp/c1_timing.py > $out/timing2.txt 2>&1
+out=gpurun_out/cg; mkdir -p $out
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_kernels.py -k "check_gather or exact or packet" > $out/pytest.log 2>&1
