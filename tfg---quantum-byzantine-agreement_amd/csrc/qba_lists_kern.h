@@ -910,7 +910,7 @@ __global__ void QBA_LISTS_BOUNDS
 // run with Philox key seed_base + i over entries [0, count).  A workgroup
 // owns whole instances, so its LDS histogram IS the instance's final count
 // and is written out directly (no slab, no reduce launch).
-template <int NP, int SAMP>
+template <int NP, int SAMP, int QPT>
 __global__ void __launch_bounds__(QBA_BLOCK)
     qba_k_batched(const QbaProgramSet *__restrict__ ps, uint64_t seed_base, int64_t n_inst,
                   uint64_t count, uint8_t *__restrict__ lists, uint64_t ld, uint64_t inst_stride,
@@ -924,14 +924,36 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
     __syncthreads();
     const uint64_t key = seed_base + (uint64_t)inst;
+    const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
     uint8_t *L = lists + (uint64_t)inst * inst_stride;
-    const uint32_t nfull = (uint32_t)count >> 2;
-    for (uint32_t q = threadIdx.x; q < nfull; q += QBA_BLOCK)
-      qba_step<NP, 1, SAMP, 1, false>(q << 2, (uint32_t)count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps, pat,
-                                   apat, thr, pl, L, ld, hist);
-    if ((count & 3) && threadIdx.x == 0)
-      qba_step<NP, 1, SAMP, 1, true>(nfull << 2, (uint32_t)count, 0, (uint32_t)key, (uint32_t)(key >> 32), ps,
-                                  pat, apat, thr, pl, L, ld, hist);
+    // QPT quads per thread-step, Q entries counted 64 at a time from the
+    // per-wave LDS queue (as qba_k_lists), then the < 4 QPT remaining entries
+    const uint32_t nunits = (uint32_t)count / (4 * QPT);
+#if QBA_QUEUE
+    QbaWaveQ wq;
+    wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
+    wq.tail = 0;
+    wq.qn = 0;
+    for (uint32_t u = threadIdx.x;; u += QBA_BLOCK) {  // wave-uniform trip count
+      const bool act = u < nunits;
+      if (!__any(act)) break;
+      qba_step<NP, 1, SAMP, QPT, false>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,
+                                        hist, &wq, act);
+    }
+    while (wq.qn) qba_q_drain<NP, true>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
+#else
+    for (uint32_t u = threadIdx.x; u < nunits; u += QBA_BLOCK)
+      qba_step<NP, 1, SAMP, QPT, false>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,
+                                        hist);
+#endif
+    const uint32_t r0 = nunits * (4 * QPT), rq = ((uint32_t)count - r0 + 3) >> 2;
+    if (threadIdx.x < rq) {
+      const uint32_t c0 = r0 + 4 * threadIdx.x;
+      if (c0 + 4 <= (uint32_t)count)
+        qba_step<NP, 1, SAMP, 1, false>(c0, (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld, hist);
+      else
+        qba_step<NP, 1, SAMP, 1, true>(c0, (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld, hist);
+    }
     __syncthreads();
     int64_t *h = H + inst * C::HB, *c = Cc + inst * C::CB, *p = P + inst * C::W;
     for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = qba_hval<NP>(hist, i);
@@ -1145,9 +1167,13 @@ int qba_launch_batched(qba_ctx *ctx, const QbaBatch &B) {
   const QbaProgramSet *hs = reinterpret_cast<const QbaProgramSet *>(ctx->prog_host[NP]);
   const int samp = sampler_of<NP>(hs);
   if (int rc = check_closed<NP>(hs)) return rc;
-  size_t lds = table_lds<NP>(hs, samp) + (size_t)C::NBINS * sizeof(uint32_t);
+  size_t lds = table_lds<NP>(hs, samp) + (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
+  if (QBA_QUEUE) lds += (size_t)(QBA_BLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
   lds = (lds + 15) & ~(size_t)15;
   const int64_t cap = (int64_t)ctx->num_cus * 16;
+  // 8-B row vectors (two quads per thread-step) when every row start allows it
+  constexpr uintptr_t VA = 4 * QBA_WIDE_QPT - 1;
+  const bool wide = !(reinterpret_cast<uintptr_t>(B.lists) & VA) && !(B.ld & VA) && !(B.inst_stride & VA);
   const int grid = (int)(B.n_inst < cap ? B.n_inst : cap);
   auto go = [&](auto kern) -> int {
     if (lds > 65536)
@@ -1159,9 +1185,12 @@ int qba_launch_batched(qba_ctx *ctx, const QbaBatch &B) {
     return QBA_OK;
   };
   if (samp == QBA_S_CLOSED) {
-    if constexpr (NP <= QBA_CLOSED_MAX_N) return go(qba_k_batched<NP, QBA_S_CLOSED>);
+    if constexpr (NP <= QBA_CLOSED_MAX_N)
+      return wide ? go(qba_k_batched<NP, QBA_S_CLOSED, QBA_WIDE_QPT>) : go(qba_k_batched<NP, QBA_S_CLOSED, 1>);
     return qba_fail(QBA_EUNSUPPORTED, "closed form beyond n = 11");
   }
-  return samp == QBA_S_FAST ? go(qba_k_batched<NP, QBA_S_FAST>) : go(qba_k_batched<NP, QBA_S_GENERAL>);
+  if (samp == QBA_S_FAST)
+    return wide ? go(qba_k_batched<NP, QBA_S_FAST, QBA_WIDE_QPT>) : go(qba_k_batched<NP, QBA_S_FAST, 1>);
+  return wide ? go(qba_k_batched<NP, QBA_S_GENERAL, QBA_WIDE_QPT>) : go(qba_k_batched<NP, QBA_S_GENERAL, 1>);
 }
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Experiment builds of libqba (n = 11 only) for A/B timing on the GPU box.
+# Experiment builds of libqba (one n: N=<n>, default 11) for A/B timing on the GPU box.
 # Usage: tools/exp/build.sh name [-DFLAG ...]
 #   SRC=<dir>  build the list kernels from another copy of csrc/ (e.g. a
 #              `git show <rev>:...` export) instead of the working tree.
@@ -7,11 +7,12 @@ set -e
 here="$(cd "$(dirname "$0")/../../tfg---quantum-byzantine-agreement_amd/csrc" && pwd)"
 src=${SRC:-$here}
 name=$1; shift
+N=${N:-11}
 out=$here/../_build/exp; mkdir -p $out
 F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -fvisibility=hidden -munsafe-fp-atomics -I$here/../../include"
-/opt/rocm/bin/hipcc $F -DQBA_ONLY_N=11 "$@" -c $src/qba_lists.hip -o $out/$name.o
-/opt/rocm/bin/hipcc $F -DQBA_INST_N=11 "$@" -c $src/qba_lists_inst.hip -o $out/${name}_n11.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/$name.so $out/$name.o $out/${name}_n11.o \
+/opt/rocm/bin/hipcc $F -DQBA_ONLY_N=$N "$@" -c $src/qba_lists.hip -o $out/$name.o
+/opt/rocm/bin/hipcc $F -DQBA_INST_N=$N "$@" -c $src/qba_lists_inst.hip -o $out/${name}_n$N.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/$name.so $out/$name.o $out/${name}_n$N.o \
   $here/../_build/qba_ctx.o $here/../_build/qba_exact.o $here/../_build/qba_sv.o $here/../_build/qba_resource.o \
   $here/../_build/qba_rccl.o $here/../_build/qba_plan.o -ldl
-rm -f $out/$name.o $out/${name}_n11.o
+rm -f $out/$name.o $out/${name}_n$N.o
