@@ -29,6 +29,23 @@ __device__ __forceinline__ uint64_t qba_ins0(uint64_t i, int b) {  // insert a 0
   return ((i >> b) << (b + 1)) | lo;
 }
 
+typedef double qba_d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 qba_ld(const double2 *p, bool nt) {
+  if (!nt) return *p;
+  const qba_d2v v = __builtin_nontemporal_load(reinterpret_cast<const qba_d2v *>(p));
+  return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ void qba_st(double2 *p, double2 v, bool nt) {
+  if (!nt) {
+    *p = v;
+    return;
+  }
+  qba_d2v w;
+  w.x = v.x;
+  w.y = v.y;
+  __builtin_nontemporal_store(w, reinterpret_cast<qba_d2v *>(p));
+}
+
 // amplitude(i) = scale * (-1)^popcount(i & minus) if (i & fixmask) == fixval,
 // else 0: |0...0> after any H/X gates on distinct untouched qubits (a fixed
 // qubit is |0> or |1>; a superposed one |+> or |-> with its sign in `minus`)
@@ -44,7 +61,7 @@ __global__ void qba_k_sv_product(double2 *__restrict__ sv, uint64_t n2, uint64_t
       const double sg = (__popcll(ik & minus) & 1) ? -scale : scale;
       v[k] = ((ik & fixmask) == fixval) ? sg : 0.0;
     }
-    sv[t] = make_double2(v[0], v[1]);
+    qba_st(sv + t, make_double2(v[0], v[1]), true);
   }
 }
 
@@ -116,6 +133,7 @@ __global__ void qba_k_sv_hset(double *__restrict__ sv, QbaHBits hb, uint64_t nth
 // not in M, else the one at (i+1)^M = (i^M) - 1 with its halves swapped.
 // Consecutive threads therefore touch contiguous bytes on both sides even
 // when M holds low bits (they only mirror the order inside a block).
+template <bool NT>
 __global__ void qba_k_sv_xmask(double *__restrict__ sv, int bc, int brep, uint64_t M, uint64_t nthreads,
                                int vec) {
   const int blo = (bc >= 0 && bc < brep) ? bc : brep, bhi = (bc >= 0 && bc < brep) ? brep : bc;
@@ -127,16 +145,14 @@ __global__ void qba_k_sv_xmask(double *__restrict__ sv, int bc, int brep, uint64
     const uint64_t j = i ^ M;
     if (vec) {
       double2 *p0 = reinterpret_cast<double2 *>(sv + i);
-      const double2 a = *p0;
+      double2 *p1 = reinterpret_cast<double2 *>(sv + ((M & 1ull) ? j - 1 : j));
+      const double2 a = qba_ld(p0, NT), c = qba_ld(p1, NT);
       if (M & 1ull) {
-        double2 *p1 = reinterpret_cast<double2 *>(sv + (j - 1));
-        const double2 c = *p1;
-        *p0 = make_double2(c.y, c.x);
-        *p1 = make_double2(a.y, a.x);
+        qba_st(p0, make_double2(c.y, c.x), NT);
+        qba_st(p1, make_double2(a.y, a.x), NT);
       } else {
-        double2 *p1 = reinterpret_cast<double2 *>(sv + j);
-        *p0 = *p1;
-        *p1 = a;
+        qba_st(p0, c, NT);
+        qba_st(p1, a, NT);
       }
     } else {
       const double a = sv[i];
@@ -278,7 +294,8 @@ static int sv_apply_fused(double *sv, int nq, const int32_t *gates, int ngates, 
       const int vec = (brep != 0 && bc != 0 && nq >= (bc >= 0 ? 3 : 2)) ? 1 : 0;
       const uint64_t npairs = (1ull << (nq - 1)) >> (bc >= 0 ? 1 : 0);
       const uint64_t nthr = npairs / (vec ? 2 : 1);
-      hipLaunchKernelGGL(qba_k_sv_xmask, dim3(sv_grid(nthr)), dim3(256), 0, s, sv, bc, brep, M, nthr, vec);
+      // nontemporal: the pass streams each line once (+2%: profiles/r2/ab11_sv_nontemporal.txt)
+      hipLaunchKernelGGL(qba_k_sv_xmask<true>, dim3(sv_grid(nthr)), dim3(256), 0, s, sv, bc, brep, M, nthr, vec);
     } else {
       bool vec = nq >= 2;
       for (int k = 0; k < r.n; ++k) vec = vec && r.cbit[k] != 0;
