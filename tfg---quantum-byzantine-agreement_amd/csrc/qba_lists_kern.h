@@ -852,13 +852,18 @@ __global__ void QBA_LISTS_BOUNDS
   // scalar load whose s_waitcnt lgkmcnt(0) also drains every LDS atomic the
   // wave has in flight (-2% step time)
   const uint32_t ustride = __builtin_amdgcn_readfirstlane(gridDim.x * BS);
+#ifdef QBA_EXP_INTERLEAVE  // experiment builds: waves interleaved across workgroups
+  const uint32_t u0 = ((threadIdx.x >> 6) * gridDim.x + blockIdx.x) * 64 + (threadIdx.x & 63);
+#else
+  const uint32_t u0 = blockIdx.x * BS + threadIdx.x;
+#endif
   if constexpr (MODE != 0 && QBA_QUEUE) {
     QbaWaveQ wq;
     wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
     wq.qn = 0;
     // wave-uniform trip count: pushes and drains always run with the whole wave
-    for (uint32_t u = blockIdx.x * BS + threadIdx.x;; u += ustride) {
+    for (uint32_t u = u0;; u += ustride) {
       const bool act = u < nunits;
       if (!__any(act)) break;
       qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
@@ -866,7 +871,7 @@ __global__ void QBA_LISTS_BOUNDS
     }
     while (wq.qn) qba_q_drain<NP, MODE == 1>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
   } else {
-    for (uint32_t u = blockIdx.x * BS + threadIdx.x; u < nunits; u += ustride)
+    for (uint32_t u = u0; u < nunits; u += ustride)
       qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
                                            lists, ld, hist);
   }
@@ -1068,6 +1073,9 @@ static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count) 
   // 1e6 entries) spreads over 163 workgroups instead of 82
   uint64_t g = (nquad + QBA_GRID_QPT * QBA_LBLOCK - 1) / (QBA_GRID_QPT * QBA_LBLOCK);
   const uint64_t cap = (uint64_t)ctx->num_cus * (uint64_t)per_cu;
+#ifdef QBA_EXP_GRID  // experiment builds: grid from the environment (QBA_EXP_GRID=<workgroups>)
+  if (const char *e = getenv("QBA_EXP_GRID")) g = strtoull(e, nullptr, 10);
+#endif
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;
