@@ -987,6 +987,9 @@ __global__ void __launch_bounds__(QBA_BLOCK)
 #ifndef QBA_RED_ROWS  // slab rows per reduce workgroup
 #define QBA_RED_ROWS 32
 #endif
+#ifndef QBA_RED_ALL_IN_FLIGHT
+#define QBA_RED_ALL_IN_FLIGHT 0
+#endif
 template <int NP>
 __global__ void __launch_bounds__(256)
     qba_k_reduce(const uint32_t *__restrict__ slab, int nrows, int64_t *__restrict__ H,
@@ -1001,6 +1004,23 @@ __global__ void __launch_bounds__(256)
     const int b0 = blockIdx.y * QBA_RED_ROWS;
     const int b1 = b0 + QBA_RED_ROWS < nrows ? b0 + QBA_RED_ROWS : nrows;
     u64 s[4] = {0ull, 0ull, 0ull, 0ull};
+#if QBA_RED_ALL_IN_FLIGHT
+    // every row's load issued before the first is summed: one memory round
+    // trip per workgroup instead of RED_ROWS / 8 (the slab was just written by
+    // the list kernel and is read from beyond L2)
+    uint4 v[QBA_RED_ROWS];
+#pragma unroll
+    for (int r = 0; r < QBA_RED_ROWS; ++r)
+      v[r] = b0 + r < b1 ? reinterpret_cast<const uint4 *>(slab + (size_t)(b0 + r) * C::NBP)[q]
+                         : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int r = 0; r < QBA_RED_ROWS; ++r) {
+      s[0] += v[r].x;
+      s[1] += v[r].y;
+      s[2] += v[r].z;
+      s[3] += v[r].w;
+    }
+#else
 #pragma unroll 8
     for (int b = b0; b < b1; ++b) {
       const uint4 v = reinterpret_cast<const uint4 *>(slab + (size_t)b * C::NBP)[q];
@@ -1009,6 +1029,7 @@ __global__ void __launch_bounds__(256)
       s[2] += v.z;
       s[3] += v.w;
     }
+#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (!s[j]) continue;
