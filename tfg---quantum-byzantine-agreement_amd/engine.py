@@ -302,7 +302,9 @@ class Engine:
         stage = np.empty(ln * (m + 1), np.int64)
         stage[:ln] = order
         if m and ln:
-            stage[ln:] = np.asarray(rows, dtype=np.int64).reshape(-1)
+            for a, t in enumerate(rows):
+                stage[ln * (a + 1):ln * (a + 2)] = t if isinstance(t, np.ndarray) else \
+                    np.fromiter(t, dtype=np.int64, count=ln)
         o = np.empty(ln + 3 + m, np.int64)
         call("qba_check_packet_host", self.ctx, _ptr(li), li.numel(), stage.ctypes.data, m, ln, int(v), int(w),
              o.ctypes.data, self.stream())

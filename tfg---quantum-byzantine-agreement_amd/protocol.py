@@ -100,16 +100,44 @@ def decide_order(Vi, v, is_comm):
 # ---------------------------------------------------------------------------
 # wire format of a (P, v, L) packet (tfg.py:199-263)
 # ---------------------------------------------------------------------------
-def send_pvl(comm, rank, dest, P, v, L, is_biz, log=None):
+def _wire(x) -> np.ndarray:
+    """int64 array of a set / tuple in its iteration order (the wire order)."""
+    return np.fromiter(x, dtype=np.int64, count=len(x))
+
+
+class WireCache:
+    """Wire arrays of the P sets and L tuples a rank handles, built once per
+    object: a packet's P and tuples are re-sent to n - 1 ranks and checked
+    once, and every conversion of a 31 K-element set or tuple costs ~0.5 ms
+    (n = 11, sizeL = 1e6).  Keyed by id(); the entry holds the object, so the
+    id cannot be reused while it is cached.  Tuples are immutable; the only
+    mutation of a P set is a dishonest rank's ``P.clear()`` (tfg.py:280), which
+    the length check catches."""
+
+    def __init__(self):
+        self._d: Dict[int, tuple] = {}
+
+    def __call__(self, x) -> np.ndarray:
+        e = self._d.get(id(x))
+        if e is None or e[0] is not x or len(e[1]) != len(x):
+            e = (x, _wire(x))
+            self._d[id(x)] = e
+        return e[1]
+
+    def put(self, x, arr: np.ndarray) -> None:
+        self._d[id(x)] = (x, arr)
+
+
+def send_pvl(comm, rank, dest, P, v, L, is_biz, log=None, wire=_wire):
     if log:
         log(f"[{'B' if is_biz else ''}{rank} -> {dest}] Sending", (P, (v, L)))
     msgs = [np.array(len(P), dtype=np.int64),
-            np.array(list(P), dtype=np.int64),
+            wire(P),
             np.array(v, dtype=np.int64),
             np.array(len(L), dtype=np.int64)]
     for sub in L:
         msgs.append(np.array(len(sub), dtype=np.int64))
-        msgs.append(np.array(sub, dtype=np.int64))
+        msgs.append(wire(sub))
     dt = _dt(comm)
     reqs = [comm.Isend([m, dt], dest=dest, tag=t) for t, m in enumerate(msgs, start=1)]
     for r in reqs:
@@ -126,16 +154,26 @@ def _recv_array(comm, src, tag, n):
     return buf
 
 
-def recv_pvl(comm, rank, src):
-    """Receive one packet; P and L are rebuilt as sets from the wire order."""
+def recv_pvl(comm, rank, src, wire: Optional["WireCache"] = None):
+    """Receive one packet; P and L are rebuilt as sets from the wire order.
+
+    Elements are Python ints (``tolist``): they hash as the reference's
+    numpy int64 scalars do, so the sets iterate in the same order, and are
+    several times cheaper to hash and convert.  A tuple's wire order is its
+    own order, so the received buffer becomes its cached wire array (P's
+    iteration order differs from the wire order: the set hop, tfg.py:209)."""
     n_p = int(_recv_array(comm, src, 1, 1)[0])
-    P = set(_recv_array(comm, src, 2, n_p))
+    P = set(_recv_array(comm, src, 2, n_p).tolist())
     v = _recv_array(comm, src, 3, 1)[0]
     n_l = int(_recv_array(comm, src, 4, 1)[0])
     L = set()
     for i in range(n_l):
         ln = int(_recv_array(comm, src, 5 + 2 * i, 1)[0])
-        L.add(tuple(_recv_array(comm, src, 6 + 2 * i, ln)))
+        buf = _recv_array(comm, src, 6 + 2 * i, ln)
+        t = tuple(buf.tolist())
+        if wire is not None:
+            wire.put(t, buf)
+        L.add(t)
     return P, v, L
 
 
@@ -189,6 +227,7 @@ class Party:
         self.dishonest = False
         self.dishonest_ids = None
         self._p_cache: Dict[int, List[int]] = {}
+        self.wire = WireCache()
         self.tolerate_empty_vi = False  # run_local: record the reference's ValueError
         self.empty_vi_error = False
 
@@ -275,19 +314,19 @@ class Party:
         if fast is None:  # engines without the fused call (the CPU test engine)
             L.add(self.own_tuple(P))
             return self.check(v, L)
-        order = np.fromiter(P, dtype=np.int64, count=len(P))
+        order = self.wire(P)
         received = list(L)
         same_len = all(len(t) == len(order) for t in received)
-        own, ok = fast(self.li, order, received if same_len else [], v, self.w)
+        own, ok = fast(self.li, order, [self.wire(t) for t in received] if same_len else [], v, self.w)
         L.add(own)
         return self._tally(ok and same_len)
 
     def send(self, dest, P, v, L):
         self.stats.sent += 1
-        send_pvl(self.comm, self.rank, dest, P, v, L, self.dishonest, self.log)
+        send_pvl(self.comm, self.rank, dest, P, v, L, self.dishonest, self.log, self.wire)
 
     def recv(self, src):
-        return recv_pvl(self.comm, self.rank, src)
+        return recv_pvl(self.comm, self.rank, src, self.wire)
 
     # tfg.py:166-196
     def comm_broadcast(self):
