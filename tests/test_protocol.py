@@ -71,3 +71,25 @@ def test_decide_order_empty_raises():
         protocol.decide_order(set(), 3, False)
     assert protocol.decide_order({4, 2}, 9, False) == 2
     assert protocol.decide_order(set(), 9, True) == 9
+
+
+def test_wire_cache_and_packet_roundtrip():
+    """protocol.WireCache: one int64 wire array per P set / L tuple object, in
+    the object's iteration order; rebuilt after the dishonest P.clear()
+    (tfg.py:280); a received tuple's buffer is reused.  recv_pvl rebuilds P
+    with Python ints whose set iterates exactly as the numpy-int64 set the
+    reference builds (tfg.py:209)."""
+    proto = sub("protocol")
+    wc = proto.WireCache()
+    rng = np.random.default_rng(3)
+    P = set(int(x) for x in rng.choice(1 << 20, 3000, replace=False))
+    a = wc(P)
+    assert a.dtype == np.int64 and list(a) == list(P) and wc(P) is a
+    P.clear()
+    assert len(wc(P)) == 0
+    t = tuple(int(x) for x in rng.integers(0, 16, 500))
+    buf = np.asarray(t, dtype=np.int64)
+    wc.put(t, buf)
+    assert wc(t) is buf
+    raw = rng.choice(1 << 30, 5000, replace=False).astype(np.int64)
+    assert list(set(raw.tolist())) == [int(x) for x in set(raw)]
