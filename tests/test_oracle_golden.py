@@ -192,3 +192,45 @@ def test_alias_table_host():
             q[i] += keep / k
             q[alias[i]] += (1 - keep) / k
         assert np.allclose(q, p / p.sum(), atol=k * 2.0 ** -31)
+
+
+_NULL_CTX_PROBE = r'''
+import ctypes as C, importlib, json, sys
+sys.path.insert(0, sys.argv[1])
+lm = importlib.import_module("tfg---quantum-byzantine-agreement_amd._lib")
+lib = lm.lib()
+skip = {"qba_last_error", "qba_version", "qba_destroy", "qba_rccl_unique_id"}
+out = {}
+for name, argt in sorted(lm.SIGNATURES.items()):
+    if name in skip:
+        continue
+    args = []
+    for t in argt:
+        if t in (C.c_double, C.c_float):
+            args.append(0.0)
+        elif t in (C.c_void_p, C.c_char_p) or hasattr(t, "contents") or getattr(t, "_type_", None) is not None and t.__name__.startswith("LP_"):
+            args.append(None)
+        else:
+            args.append(0)
+    rc = getattr(lib, name)(*args)
+    out[name] = [int(rc), lib.qba_last_error().decode()]
+print(json.dumps(out))
+'''
+
+
+def test_entry_points_reject_null_arguments():
+    """Every entry point called with a NULL context / NULL buffers / zero
+    sizes returns a negative status with a message on qba_last_error(), and
+    touches nothing (no GPU needed; run in a child process so that a crash
+    would fail this test instead of the suite)."""
+    import json as _json
+    import subprocess
+    import sys as _sys
+    r = subprocess.run([_sys.executable, "-c", _NULL_CTX_PROBE, str(ROOT)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = _json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(res) >= 28
+    for name, (rc, msg) in res.items():
+        assert rc < 0, (name, rc)
+        assert msg.startswith(name + ":"), (name, msg)
