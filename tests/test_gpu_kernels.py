@@ -625,3 +625,48 @@ def test_check_gather_vs_oracle(engine):
         engine.check_gather(lists, count, np.array([[0, 1]]), [n + 5], 0, w)
     with pytest.raises(sub("engine").QbaError):
         engine.check_gather(lists, count, np.zeros((0, 3), np.int64), [], 0, w)
+
+
+def test_invalid_arguments_leave_context_usable(engine):
+    """Malformed calls on a live context fail with QbaError (nothing launched
+    or read out of bounds), and the context keeps working afterwards: party
+    counts outside [1, 15], ld < count, missing outputs, malformed gates, nq
+    outside [1, 8], indices outside a list."""
+    lm = sub("_lib")
+    n, count = 11, 4096
+    engine.prepare(n)
+    lists = engine.sample(n, 1, 0, count)
+    ptr = lists.data_ptr()
+    s = engine.stream()
+    bad_calls = [
+        ("qba_sample", engine.ctx, 0, 1, 0, count, ptr, lists.stride(0), s),
+        ("qba_sample", engine.ctx, 16, 1, 0, count, ptr, lists.stride(0), s),
+        ("qba_sample", engine.ctx, n, 1, 0, count, ptr, count - 1, s),
+        ("qba_sample_check", engine.ctx, n, 1, 0, count, ptr, lists.stride(0), None, None, None, 0, s),
+        ("qba_check_counts", engine.ctx, n, ptr, count, count - 1, None, None, None, 0, s),
+    ]
+    for name, *args in bad_calls:
+        with pytest.raises(lm.QbaError):
+            lm.call(name, *args)
+    sv = torch.empty(1 << 4, dtype=torch.float64, device=engine.device)
+    for gates in ([(0, 4, -1)], [(0, 1, 2)], [(1, 2, 2)], [(2, 0, -1)], [(1, 0, -3)]):
+        g = np.array(gates, np.int32)
+        with pytest.raises(lm.QbaError):
+            engine.statevector(4, g, out=sv)
+        with pytest.raises(lm.QbaError):
+            engine.apply_gates(sv, 4, g)
+    raw = torch.zeros(64, dtype=torch.int64, device=engine.device)
+    vals = torch.zeros(8, dtype=torch.uint8, device=engine.device)
+    for nq in (0, 9):
+        with pytest.raises(lm.QbaError):
+            lm.call("qba_bits_to_values", engine.ctx, raw.data_ptr(), 8, nq, vals.data_ptr(), s)
+    lc = lists[1, :count].contiguous()
+    with pytest.raises(lm.QbaError):
+        engine.select_eq(np.array([0, count], np.int64), lc, 3)
+    # still usable: the same calls with valid arguments match the oracle
+    info = engine.prepare(n)
+    got, c = engine.sample_check(n, 9, 0, count)
+    ref = oracle_lib.sample(n, 9, 0, count, info["notq"], info["q"], info["closed"])
+    assert np.array_equal(got[:, :count].cpu().numpy(), ref)
+    H, C, P, _ = oracle_lib.counts(ref, n)
+    assert np.array_equal(c.numpy()[0], H)

@@ -1,3 +1,3 @@
 set -eo pipefail
-out=gpurun_out/ub; mkdir -p $out
-timeout -k 10 120 ./tools/ubench/stores2 > $out/stores2.txt 2>&1
+out=gpurun_out/inv; mkdir -p $out
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_kernels.py -k "invalid or gather" > $out/pytest.log 2>&1
