@@ -110,7 +110,8 @@ class WireCache:
     object: a packet's P and tuples are re-sent to n - 1 ranks and checked
     once, and every conversion of a 31 K-element set or tuple costs ~0.5 ms
     (n = 11, sizeL = 1e6).  Keyed by id(); the entry holds the object, so the
-    id cannot be reused while it is cached.  Tuples are immutable; the only
+    id cannot be reused while it is cached; Party.recv clears it, so it holds
+    at most the packet in hand.  Tuples are immutable; the only
     mutation of a P set is a dishonest rank's ``P.clear()`` (tfg.py:280), which
     the length check catches."""
 
@@ -126,6 +127,9 @@ class WireCache:
 
     def put(self, x, arr: np.ndarray) -> None:
         self._d[id(x)] = (x, arr)
+
+    def clear(self) -> None:
+        self._d.clear()
 
 
 def send_pvl(comm, rank, dest, P, v, L, is_biz, log=None, wire=_wire):
@@ -326,6 +330,10 @@ class Party:
         send_pvl(self.comm, self.rank, dest, P, v, L, self.dishonest, self.log, self.wire)
 
     def recv(self, src):
+        # a packet is checked and re-sent before the next one is received, so
+        # the cache only ever needs the packet in hand: dropping the previous
+        # one keeps memory at one packet (a 1e7-entry P set is ~20 MB)
+        self.wire.clear()
         return recv_pvl(self.comm, self.rank, src, self.wire)
 
     # tfg.py:166-196

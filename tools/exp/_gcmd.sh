@@ -1,3 +1,5 @@
 set -eo pipefail
-out=gpurun_out/inv; mkdir -p $out
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_kernels.py -k "invalid or gather" > $out/pytest.log 2>&1
+out=gpurun_out/full2; mkdir -p $out
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $out/pytest.log 2>&1
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
+timeout -k 10 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench.json 2> $out/bench.err
