@@ -277,7 +277,8 @@ def config0(args, eng):
     host's in-process world, exact-order checks on the GPU engine."""
     protocol = importlib.import_module(f"{PKG}.protocol")
     runs = []
-    protocol.run_local(3, 1000, 1, eng, seed=1)  # warm (compiles n=3)
+    for s in range(max(1, args.warmup)):  # warm: compiles n=3, grows the staging buffers
+        protocol.run_local(3, 1000, 1, eng, seed=1000 + s)
     t0 = time.perf_counter()
     for s in range(args.steps):
         runs.append(protocol.run_local(3, 1000, 1, eng, seed=1 + s))
