@@ -10,6 +10,7 @@ out=$root/gpurun_out/$tag; mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o bench -- \
     python $root/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $out/trace_bench.json 2> $out/trace.log
+python $root/tools/trace_check.py $out/trace $out/trace_bench.json > $out/trace_check.txt
 bash $root/tools/pmc.sh gpurun_out/$tag/pmc
 python $root/tools/pmc_summary.py $out/pmc > $out/pmc_summary.txt
 python $root/tools/pmc_traffic.py $out/pmc 125000000 11 > $out/traffic_n11.json
