@@ -1,5 +1,6 @@
 set -eo pipefail
-out=gpurun_out/full2; mkdir -p $out
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $out/pytest.log 2>&1
-timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
-timeout -k 10 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench.json 2> $out/bench.err
+out=gpurun_out/pre; mkdir -p $out
+E=$PWD/tfg---quantum-byzantine-agreement_amd/_build/exp
+QBA_LIB=$E/b_pre.so timeout -k 10 200 python tools/exp/parity11.py > $out/parity_b_pre.txt 2>&1
+ROUNDS=2 timeout -k 10 600 bash tools/exp/ab_c1.sh pre
+ROUNDS=1 timeout -k 10 600 bash tools/exp/ab.sh pre_h
