@@ -15,10 +15,11 @@
 //    (qba_k_sv_hset: each thread owns the 2^K amplitudes of one coset);
 //  * a window of pairwise-commuting X / CX gates is one XOR pass: a single
 //    control (or none) -> qba_k_sv_xmask, several -> qba_k_sv_xmulti.
-// Threads access 16 B (a double2) whenever bit 0 lets them, and consecutive
-// threads touch consecutive addresses on every access, so each pass is bound
-// by HBM at 16 B of traffic per amplitude it moves (8 read + 8 written; the
-// product pass writes 8 B per amplitude and reads nothing).
+// Threads access 16 B (a double2) whenever bit 0 lets them, and a wave's
+// access covers contiguous bytes (half-dense only when bits 0 and 1 are both
+// in an H set), so each pass is bound by HBM at 16 B of traffic per amplitude
+// it moves (8 read + 8 written; the product pass writes 8 B per amplitude and
+// reads nothing); the streaming passes use nontemporal accesses.
 #include "qba_compact.h"
 
 static constexpr double kInvSqrt2 = 0.70710678118654752440;
