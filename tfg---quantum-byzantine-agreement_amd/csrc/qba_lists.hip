@@ -75,14 +75,19 @@ static int dispatch_one(qba_ctx *ctx, const QbaLaunch &L) {
   }
 }
 
-// Launches of at most QBA_CHUNK entries (32-bit in-kernel offsets, u32 bins);
-// chunks after the first accumulate into the caller's counts.
+// Launches of at most QBA_CHUNK entries (32-bit in-kernel offsets, u32 bins)
+// that never cross a multiple of 2^33 entries (inside a launch the high word
+// of the Philox pair counter e >> 1 is constant: qba_sample_quad keeps it in
+// an SGPR); chunks after the first accumulate into the caller's counts.
 static int dispatch(qba_ctx *ctx, const QbaLaunch &L0) {
   QbaLaunch L = L0;
   uint64_t done = 0;
   int rc = QBA_OK;
+  constexpr uint64_t PHI_SPAN = 1ull << 33;
   do {
     L.count = L0.count - done < ctx->chunk ? L0.count - done : ctx->chunk;
+    const uint64_t to_span = PHI_SPAN - ((L0.first + done) & (PHI_SPAN - 1));
+    if (L.count > to_span) L.count = to_span;
     L.first = L0.first + done;
     L.lists = L0.lists + done;
     L.accumulate = done ? 1 : L0.accumulate;

@@ -33,6 +33,21 @@
 #ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
 #define QBA_NT_STORE 1
 #endif
+#ifndef QBA_PHI_UNIFORM  // closed-form quads: Philox counter high word in an SGPR
+#define QBA_PHI_UNIFORM 1
+#endif
+#ifndef QBA_SEL_BITOP3  // closed-form finish: Q / not-Q select as one v_bitop3 per word
+#define QBA_SEL_BITOP3 1
+#endif
+#ifndef QBA_STAGE_VEC  // stage tables -> LDS with 16-B loads issued together
+#define QBA_STAGE_VEC 1
+#endif
+#ifndef QBA_ISQ_ROWS  // fused kernel: isQCorr of a quad from its transposed rows 0 and 1
+#define QBA_ISQ_ROWS 0
+#endif
+#ifndef QBA_NQ2  // closed-form not-Q values straight from the nibble words (schedule v2)
+#define QBA_NQ2 0
+#endif
 
 
 template <int NP>
@@ -272,11 +287,22 @@ template <int NP>
 __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
                                                 uint32_t k0, uint32_t k1, QbaClosed &c) {
   using F = CF<NP>;
+#if QBA_NQ2
+  // groups 1..3 = nibbles 1..3 of w1's low nibbles (group 0 = group 1),
+  // groups 4..7 = w1's high nibbles, groups 8..11 = w0's high nibbles: the
+  // words ARE the byte layout, one v_perm in all
+  const uint32_t a = w1 & F::M4;
+  c.nq[0] = qba_perm_b(a, a, 0x03020101u);
+  c.nq[1] = (w1 >> 4) & F::M4;
+  c.nq[2] = (w0 >> 4) & F::M4;
+  c.nq[3] = 0u;
+#else
   const uint32_t a = w1 & F::M4, b = (w1 >> 4) & F::M4, cc = (w0 >> 8) & F::M4, d = (w0 >> 12) & F::M4;
   c.nq[0] = qba_perm_b(a, a, 0x02010000u);
   c.nq[1] = qba_perm_b(b, a, 0x06050403u);
   c.nq[2] = qba_perm_b(cc, b, 0x06050403u);
   c.nq[3] = qba_perm_b(d, cc, 0x06050403u);
+#endif
   c.w0 = w0;
   const bool o1 = qba_accept<NP>(w1, F::T32);
   uint32_t rank = o1 ? w1 : (w0 & ~31u);
@@ -309,9 +335,19 @@ __device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint
   q[F::WIN] = y0;
   q[F::WIN + 1] = y1;
   const uint32_t R = ((c.w0 >> 1) & (uint32_t)(QCfg<NP>::W - 1)) * 0x01010101u;
+#if QBA_SEL_BITOP3
+  // all ones for a Q-correlated entry: one v_bfe_i32, opaque so that each
+  // word's select stays one v_bitop3 (qm ? q ^ R : nq) instead of and + cmp
+  // for a mask plus a v_cndmask per word
+  uint32_t qm = (uint32_t)__builtin_amdgcn_sbfe((int)c.w0, 0, 1);
+  asm("" : "+v"(qm));
+#pragma unroll
+  for (int i = 0; i < F::ND; ++i) D[i] = (qm & (q[i] ^ R)) | (~qm & c.nq[i]);
+#else
   const uint32_t qm = 0u - (c.w0 & 1u);  // all ones for a Q-correlated entry
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) D[i] = c.nq[i] ^ ((q[i] ^ R ^ c.nq[i]) & qm);
+#endif
 }
 
 // Stage table indices of a rank and the LDS reads.
@@ -529,12 +565,26 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
   constexpr int ND = CF<NP>::ND;
   if constexpr (SAMP == QBA_S_CLOSED && !TAIL) {
     if (!(first & 1)) {  // wave-uniform: the quad is two whole pairs
-      const uint64_t p0 = (first + c0) >> 1;
       QbaClosed cl[4];
+#if QBA_PHI_UNIFORM
+      // A launch never crosses a multiple of 2^33 entries (dispatch splits
+      // there), so the pair counter's high word is the launch's and the low
+      // word never carries: p_hi stays in an SGPR, Philox's round 1 and half
+      // of round 2 are scalar.
+      const uint32_t phi = (uint32_t)(first >> 33);
+      const uint32_t plo = (uint32_t)(first >> 1) + (c0 >> 1);
+#else
+      const uint64_t p0 = (first + c0) >> 1;
+#endif
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
+#if QBA_PHI_UNIFORM
+        const uint64_t p = ((uint64_t)phi << 32) | (uint64_t)(plo + (uint32_t)jp);
+        const QbaU4 x = qba_philox(plo + (uint32_t)jp, phi, 0u, 0u, k0, k1);
+#else
         const uint64_t p = p0 + jp;
         const QbaU4 x = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0u, 0u, k0, k1);
+#endif
         qba_closed_rank<NP>(x.x, x.y, p, 0u, k0, k1, cl[2 * jp]);
         qba_closed_rank<NP>(x.z, x.w, p, 1u, k0, k1, cl[2 * jp + 1]);
       }
@@ -734,8 +784,16 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
                row[k][4 * i + 2], row[k][4 * i + 3]);
       if constexpr (MODE == 1) {
         if (wq) {
+#if QBA_ISQ_ROWS
+          // L0 != L1 (tfg.py:327) of the quad's 4 entries at once: byte j of
+          // row 0 XOR row 1 is nonzero iff entry j is Q-correlated
+          const uint32_t xq = (row[k][0] ^ row[k][1]) & (act ? 0xffffffffu : 0u);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) qba_q_push<NP, MODE == 1>(*wq, D[j], (xq & (0xffu << (8 * j))) != 0u, hist);
+#else
 #pragma unroll
           for (int j = 0; j < 4; ++j) qba_q_push<NP, MODE == 1>(*wq, D[j], qba_isq_d<NP>(D[j], am), hist);
+#endif
         } else {
           qba_count_quad<NP>(D, valid, hist, row[k]);
         }
@@ -780,7 +838,23 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
+#if QBA_STAGE_VEC
+    // 16-B loads, all issued before the first LDS write: one memory round
+    // trip per workgroup instead of one per word-loop iteration (the image
+    // pads the tables to whole 16-B words, qba_plan_image)
+    constexpr int W4 = (CF<NP>::WORDS + 3) / 4, PER = (W4 + BS - 1) / BS;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    uint4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (threadIdx.x + k * BS < W4) v[k] = s4[threadIdx.x + k * BS];
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (threadIdx.x + k * BS < W4) d4[threadIdx.x + k * BS] = v[k];
+#else
     for (int i = threadIdx.x; i < CF<NP>::WORDS; i += BS) dst[i] = src[i];
+#endif
     hist = dst + ((CF<NP>::WORDS + 3) & ~3);
   } else if constexpr (MODE != 2) {
     const int T = ps->table_total;

@@ -326,8 +326,10 @@ int qba_plan_image(int n, const QbaHostProgram &a, const QbaHostProgram &b, std:
   int offB = 0, offC = 0;
   if (closed) build_perm_tables(n, pw, ra, rb, rc, offB, offC);
   if (pw.size() > QBA_PERM_MAX_WORDS) return qba_fail(QBA_EINVAL, "permutation tables too large");
-  const size_t perm_off = sizeof(QbaProgramSet) + 3 * sizeof(uint64_t) * (size_t)T;
-  img.assign(perm_off + sizeof(uint32_t) * pw.size(), 0);
+  // stage tables 16-B aligned and padded to whole 16-B words: the list kernels
+  // stage them into LDS with 16-B loads
+  const size_t perm_off = (sizeof(QbaProgramSet) + 3 * sizeof(uint64_t) * (size_t)T + 15) & ~(size_t)15;
+  img.assign(perm_off + sizeof(uint32_t) * ((pw.size() + 3) & ~(size_t)3), 0);
   QbaProgramSet *ps = reinterpret_cast<QbaProgramSet *>(img.data());
   ps->prog[0] = a.p;
   ps->prog[1] = b.p;
