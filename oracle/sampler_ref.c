@@ -173,11 +173,13 @@ static void closed_entry(int n, uint64_t seed, uint64_t e, uint8_t vals[16]) {
   const int nq = n_qubits(n);
   const uint32_t W = 1u << nq;
   if (!(w0 & 1u)) { /* not-Q: L0 = L1, L1..Ln independent uniform */
-    static const int w1_shift[8] = {0, 8, 16, 24, 4, 12, 20, 28};
-    static const int w0_shift[6] = {8, 16, 24, 12, 20, 28};
-    uint32_t v[14];
-    for (int i = 0; i < 8; ++i) v[i] = (w1 >> w1_shift[i]) & (W - 1);
-    for (int i = 0; i < 6; ++i) v[8 + i] = (w0 >> w0_shift[i]) & (W - 1);
+    /* group g >= 1 takes v[g - 1]: w1's low nibbles 1..3, w1's high nibbles,
+     * w0's high nibbles (w0's low nibbles hold isQ and r of a Q entry) */
+    static const int w1_shift[7] = {8, 16, 24, 4, 12, 20, 28};
+    static const int w0_shift[4] = {4, 12, 20, 28};
+    uint32_t v[11];
+    for (int i = 0; i < 7; ++i) v[i] = (w1 >> w1_shift[i]) & (W - 1);
+    for (int i = 0; i < 4; ++i) v[7 + i] = (w0 >> w0_shift[i]) & (W - 1);
     vals[0] = (uint8_t)v[0];
     for (int g = 1; g <= n; ++g) vals[g] = (uint8_t)v[g - 1];
     return;

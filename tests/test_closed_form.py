@@ -80,8 +80,10 @@ def closed_entry_py(n, seed, e):
     x = [int(v) for v in oracle_lib.philox(np.array([p & 0xFFFFFFFF, p >> 32, 0, 0], np.uint32), seed)[0]]
     w0, w1 = x[2 * h], x[2 * h + 1]
     if not w0 & 1:
-        vals = [(w1 >> s) & (W - 1) for s in (0, 8, 16, 24, 4, 12, 20, 28)] + \
-               [(w0 >> s) & (W - 1) for s in (8, 16, 24, 12, 20, 28)]
+        # group g >= 1: nibble g of the word pair (w1 low nibbles, w1 high
+        # nibbles, w0 high nibbles, byte order); group 0 = group 1
+        vals = [(w1 >> s) & (W - 1) for s in (8, 16, 24, 4, 12, 20, 28)] + \
+               [(w0 >> s) & (W - 1) for s in (4, 12, 20, 28)]
         return [vals[0]] + vals[: n]
     nf = math.factorial(n)
     t32, t27 = (1 << 32) % nf, ((1 << 27) % nf) << 5

@@ -491,6 +491,25 @@ def test_chunked_launches(monkeypatch):
         eng.close()
 
 
+@pytest.mark.parametrize("n,first,count", [(11, (1 << 33) - 4000, 12_008), (11, (1 << 34) - 3, 20_001),
+                                           (7, (3 << 33) - 8, 16)])
+def test_launch_split_at_counter_word(engine, n, first, count):
+    """A launch never crosses a multiple of 2^33 entries (the high word of the
+    Philox pair counter e >> 1 is uniform inside a launch): a call across one
+    is split there, and lists and counts still equal the C twin's."""
+    seed = 0xC0FFEE + n
+    info = engine.prepare(n)
+    lists, counts = engine.sample_check(n, seed, first, count)
+    torch.cuda.synchronize()
+    got = lists[:, :count].cpu().numpy()
+    ref = oracle_lib.sample(n, seed, first, count, info["notq"], info["q"], info["closed"])
+    assert np.array_equal(got, ref)
+    H, C, P, _ = oracle_lib.counts(ref, n)
+    gH, gC, gP = counts.numpy()
+    assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+    assert np.array_equal(engine.sample(n, seed, first, count)[:, :count].cpu().numpy(), ref)
+
+
 def test_counts_repeated_accumulate_stats():
     """The count reduction (slab rows + qba_k_reduce) against the oracle on a
     fresh context: several n, repeated launches, accumulation, check-only

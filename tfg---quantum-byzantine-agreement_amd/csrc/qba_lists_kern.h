@@ -43,10 +43,10 @@
 #define QBA_STAGE_VEC 1
 #endif
 #ifndef QBA_ISQ_ROWS  // fused kernel: isQCorr of a quad from its transposed rows 0 and 1
-#define QBA_ISQ_ROWS 0
+#define QBA_ISQ_ROWS 1
 #endif
-#ifndef QBA_NQ2  // closed-form not-Q values straight from the nibble words (schedule v2)
-#define QBA_NQ2 0
+#ifndef QBA_ROW_SADDR  // row stores with an SGPR row base and a 32-bit lane offset
+#define QBA_ROW_SADDR 1
 #endif
 
 
@@ -209,8 +209,8 @@ __device__ __forceinline__ typename QCfg<NP>::Out qba_sample_entry_fast(
 // pairs: entry e uses half h = e & 1 of block
 //   x = philox(ctr = {p_lo, p_hi, 0, 0}, key = seed),  p = e >> 1,
 // i.e. the 64 bits w0 = x[2h], w1 = x[2h+1].  isQ = w0 & 1.
-//   not-Q: values v_0..v_13 = the nQ low bits of the nibbles at bits
-//          {0,8,16,24, 4,12,20,28} of w1 then {8,16,24, 12,20,28} of w0;
+//   not-Q: values v_0..v_10 = the nQ low bits of the nibbles at bits
+//          {8,16,24, 4,12,20,28} of w1 then {4,12,20,28} of w0;
 //          group g >= 1 takes v_{g-1}, group 0 takes v_0 (= group 1,
 //          tfg.py:15-22).
 //   Q:     r = (w0 >> 1) & (W-1).  The rank word F is w1 if
@@ -287,22 +287,14 @@ template <int NP>
 __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
                                                 uint32_t k0, uint32_t k1, QbaClosed &c) {
   using F = CF<NP>;
-#if QBA_NQ2
-  // groups 1..3 = nibbles 1..3 of w1's low nibbles (group 0 = group 1),
-  // groups 4..7 = w1's high nibbles, groups 8..11 = w0's high nibbles: the
-  // words ARE the byte layout, one v_perm in all
+  // group g >= 1 = nibble g of (w1 low nibbles, w1 high nibbles, w0 high
+  // nibbles) in byte order, group 0 = group 1: the masked words ARE the byte
+  // layout, one v_perm in all (w0's low nibbles carry isQ and r)
   const uint32_t a = w1 & F::M4;
   c.nq[0] = qba_perm_b(a, a, 0x03020101u);
   c.nq[1] = (w1 >> 4) & F::M4;
   c.nq[2] = (w0 >> 4) & F::M4;
   c.nq[3] = 0u;
-#else
-  const uint32_t a = w1 & F::M4, b = (w1 >> 4) & F::M4, cc = (w0 >> 8) & F::M4, d = (w0 >> 12) & F::M4;
-  c.nq[0] = qba_perm_b(a, a, 0x02010000u);
-  c.nq[1] = qba_perm_b(b, a, 0x06050403u);
-  c.nq[2] = qba_perm_b(cc, b, 0x06050403u);
-  c.nq[3] = qba_perm_b(d, cc, 0x06050403u);
-#endif
   c.w0 = w0;
   const bool o1 = qba_accept<NP>(w1, F::T32);
   uint32_t rank = o1 ? w1 : (w0 & ~31u);
@@ -811,7 +803,18 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
         uint32_t *pv = reinterpret_cast<uint32_t *>(&v);
 #pragma unroll
         for (int k = 0; k < QPT; ++k) pv[k] = row[k][g];
+#if QBA_ROW_SADDR
+        // row base opaque in SGPRs (an empty asm: no instruction is emitted),
+        // so the store is `global_store v_c0, v_data, s[row]` with a 32-bit
+        // lane offset -- otherwise the compiler shares lists + c0 as a 64-bit
+        // VGPR and pays a 64-bit VALU add per row
+        uint64_t rb = reinterpret_cast<uint64_t>(lists) + (uint64_t)g * ld;
+        asm("" : "+s"(rb));
+        typedef __attribute__((address_space(1))) V GV;  // global, not flat
+        GV *dst = reinterpret_cast<GV *>(rb + c0);
+#else
         V *dst = reinterpret_cast<V *>(lists + (uint64_t)g * ld + c0);
+#endif
 #if QBA_NT_STORE
         // the rows are streamed out once: nontemporal stores move the 12 rows of
         // 1.25e8 entries in 0.313 ms instead of 0.356 (tools/ubench/stores2)
