@@ -45,6 +45,9 @@
 #ifndef QBA_ISQ_ROWS  // fused kernel: isQCorr of a quad from its transposed rows 0 and 1
 #define QBA_ISQ_ROWS 1
 #endif
+#ifndef QBA_QTWEAK  // queue push / drain address arithmetic without a per-use v_mov
+#define QBA_QTWEAK 1
+#endif
 #ifndef QBA_ROW_SADDR  // row stores with an SGPR row base and a 32-bit lane offset
 #define QBA_ROW_SADDR 1
 #endif
@@ -463,7 +466,8 @@ __device__ __forceinline__ uint32_t qba_byte_of(int g, uint32_t w0, uint32_t w1,
 // ---------------------------------------------------------------------------
 template <int NP>
 __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uint32_t one,
-                                            uint32_t *hist, bool in_range, bool known_q = false) {
+                                            uint32_t *hist, bool in_range, bool known_q = false,
+                                            uint32_t hoff = 0xffffffffu) {
   using C = QCfg<NP>;
   using F = CF<NP>;
   const uint32_t l0 = D[0] & 0xffu, l1 = (D[0] >> 8) & 0xffu;
@@ -485,7 +489,10 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
     atomicAdd(&hist[C::HBL + C::CBL + 0], 1u);
     return;
   }
-  const uint32_t hb = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist + l1 * (uint32_t)(C::G * C::WP * 4);
+  // hoff: the histogram's LDS byte address held in a VGPR by the caller (the
+  // row base is then one v_mad_u32_u24 with the stride in an SGPR)
+  if (hoff == 0xffffffffu) hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
+  const uint32_t hb = hoff + l1 * (uint32_t)(C::G * C::WP * 4);
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) {
     const uint32_t E = D[i] << 2;  // byte b = 4 * value (< 64: no carry into the next byte)
@@ -659,6 +666,7 @@ __device__ __forceinline__ bool qba_isq_d(const uint32_t (&D)[CF<NP>::ND], uint3
 struct QbaWaveQ {
   uint32_t base;      // LDS byte address of this wave's ring [ND][QBA_QCAP] words (aligned to 4 QBA_QCAP B)
   uint32_t tail, qn;  // wave-uniform: first queued slot (not reduced mod QBA_QCAP), queued entries
+  uint32_t hoff;      // LDS byte address of the histogram, kept in a VGPR (see qba_count_d)
 };
 
 // LDS byte address of ring slot s (any integer: taken mod QBA_QCAP); the
@@ -689,7 +697,7 @@ __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_
   uint32_t D[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) D[i] = *qba_lds(a + i * QBA_QCAP * 4);
-  if (nv >= 64 || lane < nv) qba_count_d<NP>(D, 0x00010001u, hist, TRUSTED, true);
+  if (nv >= 64 || lane < nv) qba_count_d<NP>(D, 0x00010001u, hist, TRUSTED, true, q.hoff);
   q.tail += nv;
   q.qn -= nv;
 }
@@ -702,10 +710,18 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
                                            uint32_t *hist) {
   constexpr int ND = CF<NP>::ND;
   const uint64_t m = __ballot(isq);
+#if QBA_QTWEAK
+  // mbcnt from 0 and the wave-uniform base added with the slot-to-byte shift
+  // (one v_add_lshl_u32): no v_mov of the base into a VGPR per push
+  const uint32_t mb = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (isq) {
+    const uint32_t a = (((mb + q.tail + q.qn) << 2) & (uint32_t)(QBA_QCAP * 4 - 1)) | q.base;
+#else
   const uint32_t slot =
       __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, q.tail + q.qn));
   if (isq) {
     const uint32_t a = qba_q_addr(q, slot);
+#endif
 #pragma unroll
     for (int i = 0; i < ND; ++i) *qba_lds(a + i * QBA_QCAP * 4) = D[i];
   }
@@ -939,6 +955,8 @@ __global__ void QBA_LISTS_BOUNDS
     wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
     wq.qn = 0;
+    wq.hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
+    asm("" : "+v"(wq.hoff));  // held in a VGPR (no instruction is emitted)
     // wave-uniform trip count: pushes and drains always run with the whole wave
     for (uint32_t u = u0;; u += ustride) {
       const bool act = u < nunits;
@@ -1016,6 +1034,8 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
     wq.qn = 0;
+    wq.hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
+    asm("" : "+v"(wq.hoff));
     for (uint32_t u = threadIdx.x;; u += QBA_BLOCK) {  // wave-uniform trip count
       const bool act = u < nunits;
       if (!__any(act)) break;
