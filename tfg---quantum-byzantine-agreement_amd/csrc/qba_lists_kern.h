@@ -48,6 +48,9 @@
 #ifndef QBA_QTWEAK  // queue push / drain address arithmetic without a per-use v_mov
 #define QBA_QTWEAK 1
 #endif
+#ifndef QBA_TAB_BCAST  // not-Q entries read stage-table entry 0 (LDS broadcast)
+#define QBA_TAB_BCAST 1
+#endif
 #ifndef QBA_ROW_SADDR  // row stores with an SGPR row base and a 32-bit lane offset
 #define QBA_ROW_SADDR 1
 #endif
@@ -314,6 +317,12 @@ __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64
         }
     }
   }
+#if QBA_TAB_BCAST
+  // a not-Q entry discards its table words (qba_closed_finish selects its
+  // nibbles): rank 0 sends its three reads to one address per table, served
+  // as an LDS broadcast, so only the Q lanes' random reads meet bank conflicts
+  rank &= (uint32_t)__builtin_amdgcn_sbfe((int)w0, 0, 1);
+#endif
   c.rank = rank;
 }
 
