@@ -98,9 +98,10 @@ def test_program_registers_large_n(engine, n):
             assert total_bits == n * nq  # L0 = L1 and L1..Ln free
 
 
-@pytest.mark.parametrize("n,first,count", [(1, 0, 1001), (2, 7, 999), (3, 0, 4096), (5, 3, 777),
-                                           (7, 1 << 33, 5003), (11, 0, 100_003), (11, (1 << 40) + 5, 20_001),
-                                           (13, 99, 3000), (15, 1, 8191)])
+@pytest.mark.parametrize("n,first,count", [(1, 0, 1001), (2, 7, 999), (3, 0, 4096), (4, 1, 30_001),
+                                           (5, 3, 777), (6, 0, 30_000), (7, 1 << 33, 5003), (8, 2, 40_003),
+                                           (9, 5, 40_000), (10, 0, 50_001), (11, 0, 100_003),
+                                           (11, (1 << 40) + 5, 20_001), (13, 99, 3000), (15, 1, 8191)])
 def test_sampler_bit_exact(engine, n, first, count):
     seed = 0x5EED ^ (n << 20)
     info = engine.prepare(n)
