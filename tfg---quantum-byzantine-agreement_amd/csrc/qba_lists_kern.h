@@ -33,27 +33,6 @@
 #ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
 #define QBA_NT_STORE 1
 #endif
-#ifndef QBA_PHI_UNIFORM  // closed-form quads: Philox counter high word in an SGPR
-#define QBA_PHI_UNIFORM 1
-#endif
-#ifndef QBA_SEL_BITOP3  // closed-form finish: Q / not-Q select as one v_bitop3 per word
-#define QBA_SEL_BITOP3 1
-#endif
-#ifndef QBA_STAGE_VEC  // stage tables -> LDS with 16-B loads issued together
-#define QBA_STAGE_VEC 1
-#endif
-#ifndef QBA_ISQ_ROWS  // fused kernel: isQCorr of a quad from its transposed rows 0 and 1
-#define QBA_ISQ_ROWS 1
-#endif
-#ifndef QBA_QTWEAK  // queue push / drain address arithmetic without a per-use v_mov
-#define QBA_QTWEAK 1
-#endif
-#ifndef QBA_TAB_BCAST  // not-Q entries read stage-table entry 0 (LDS broadcast)
-#define QBA_TAB_BCAST 1
-#endif
-#ifndef QBA_ROW_SADDR  // row stores with an SGPR row base and a 32-bit lane offset
-#define QBA_ROW_SADDR 1
-#endif
 
 
 template <int NP>
@@ -317,12 +296,10 @@ __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64
         }
     }
   }
-#if QBA_TAB_BCAST
   // a not-Q entry discards its table words (qba_closed_finish selects its
   // nibbles): rank 0 sends its three reads to one address per table, served
   // as an LDS broadcast, so only the Q lanes' random reads meet bank conflicts
   rank &= (uint32_t)__builtin_amdgcn_sbfe((int)w0, 0, 1);
-#endif
   c.rank = rank;
 }
 
@@ -339,7 +316,6 @@ __device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint
   q[F::WIN] = y0;
   q[F::WIN + 1] = y1;
   const uint32_t R = ((c.w0 >> 1) & (uint32_t)(QCfg<NP>::W - 1)) * 0x01010101u;
-#if QBA_SEL_BITOP3
   // all ones for a Q-correlated entry: one v_bfe_i32, opaque so that each
   // word's select stays one v_bitop3 (qm ? q ^ R : nq) instead of and + cmp
   // for a mask plus a v_cndmask per word
@@ -347,11 +323,6 @@ __device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint
   asm("" : "+v"(qm));
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) D[i] = (qm & (q[i] ^ R)) | (~qm & c.nq[i]);
-#else
-  const uint32_t qm = 0u - (c.w0 & 1u);  // all ones for a Q-correlated entry
-#pragma unroll
-  for (int i = 0; i < F::ND; ++i) D[i] = c.nq[i] ^ ((q[i] ^ R ^ c.nq[i]) & qm);
-#endif
 }
 
 // Stage table indices of a rank and the LDS reads.
@@ -574,25 +545,16 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
   if constexpr (SAMP == QBA_S_CLOSED && !TAIL) {
     if (!(first & 1)) {  // wave-uniform: the quad is two whole pairs
       QbaClosed cl[4];
-#if QBA_PHI_UNIFORM
       // A launch never crosses a multiple of 2^33 entries (dispatch splits
       // there), so the pair counter's high word is the launch's and the low
       // word never carries: p_hi stays in an SGPR, Philox's round 1 and half
       // of round 2 are scalar.
       const uint32_t phi = (uint32_t)(first >> 33);
       const uint32_t plo = (uint32_t)(first >> 1) + (c0 >> 1);
-#else
-      const uint64_t p0 = (first + c0) >> 1;
-#endif
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
-#if QBA_PHI_UNIFORM
         const uint64_t p = ((uint64_t)phi << 32) | (uint64_t)(plo + (uint32_t)jp);
         const QbaU4 x = qba_philox(plo + (uint32_t)jp, phi, 0u, 0u, k0, k1);
-#else
-        const uint64_t p = p0 + jp;
-        const QbaU4 x = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0u, 0u, k0, k1);
-#endif
         qba_closed_rank<NP>(x.x, x.y, p, 0u, k0, k1, cl[2 * jp]);
         qba_closed_rank<NP>(x.z, x.w, p, 1u, k0, k1, cl[2 * jp + 1]);
       }
@@ -719,18 +681,11 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
                                            uint32_t *hist) {
   constexpr int ND = CF<NP>::ND;
   const uint64_t m = __ballot(isq);
-#if QBA_QTWEAK
   // mbcnt from 0 and the wave-uniform base added with the slot-to-byte shift
   // (one v_add_lshl_u32): no v_mov of the base into a VGPR per push
   const uint32_t mb = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
   if (isq) {
     const uint32_t a = (((mb + q.tail + q.qn) << 2) & (uint32_t)(QBA_QCAP * 4 - 1)) | q.base;
-#else
-  const uint32_t slot =
-      __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, q.tail + q.qn));
-  if (isq) {
-    const uint32_t a = qba_q_addr(q, slot);
-#endif
 #pragma unroll
     for (int i = 0; i < ND; ++i) *qba_lds(a + i * QBA_QCAP * 4) = D[i];
   }
@@ -801,16 +756,11 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
                row[k][4 * i + 2], row[k][4 * i + 3]);
       if constexpr (MODE == 1) {
         if (wq) {
-#if QBA_ISQ_ROWS
           // L0 != L1 (tfg.py:327) of the quad's 4 entries at once: byte j of
           // row 0 XOR row 1 is nonzero iff entry j is Q-correlated
           const uint32_t xq = (row[k][0] ^ row[k][1]) & (act ? 0xffffffffu : 0u);
 #pragma unroll
           for (int j = 0; j < 4; ++j) qba_q_push<NP, MODE == 1>(*wq, D[j], (xq & (0xffu << (8 * j))) != 0u, hist);
-#else
-#pragma unroll
-          for (int j = 0; j < 4; ++j) qba_q_push<NP, MODE == 1>(*wq, D[j], qba_isq_d<NP>(D[j], am), hist);
-#endif
         } else {
           qba_count_quad<NP>(D, valid, hist, row[k]);
         }
@@ -828,7 +778,6 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
         uint32_t *pv = reinterpret_cast<uint32_t *>(&v);
 #pragma unroll
         for (int k = 0; k < QPT; ++k) pv[k] = row[k][g];
-#if QBA_ROW_SADDR
         // row base opaque in SGPRs (an empty asm: no instruction is emitted),
         // so the store is `global_store v_c0, v_data, s[row]` with a 32-bit
         // lane offset -- otherwise the compiler shares lists + c0 as a 64-bit
@@ -837,9 +786,6 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
         asm("" : "+s"(rb));
         typedef __attribute__((address_space(1))) V GV;  // global, not flat
         GV *dst = reinterpret_cast<GV *>(rb + c0);
-#else
-        V *dst = reinterpret_cast<V *>(lists + (uint64_t)g * ld + c0);
-#endif
 #if QBA_NT_STORE
         // the rows are streamed out once: nontemporal stores move the 12 rows of
         // 1.25e8 entries in 0.313 ms instead of 0.356 (tools/ubench/stores2)
@@ -866,7 +812,6 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
-#if QBA_STAGE_VEC
     // 16-B loads, all issued before the first LDS write: one memory round
     // trip per workgroup instead of one per word-loop iteration (the image
     // pads the tables to whole 16-B words, qba_plan_image)
@@ -880,9 +825,6 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
 #pragma unroll
     for (int k = 0; k < PER; ++k)
       if (threadIdx.x + k * BS < W4) d4[threadIdx.x + k * BS] = v[k];
-#else
-    for (int i = threadIdx.x; i < CF<NP>::WORDS; i += BS) dst[i] = src[i];
-#endif
     hist = dst + ((CF<NP>::WORDS + 3) & ~3);
   } else if constexpr (MODE != 2) {
     const int T = ps->table_total;
