@@ -1,5 +1,5 @@
 set -eo pipefail
-out=gpurun_out/r2d; mkdir -p $out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/pytest.log 2>&1
-timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
-timeout -k 10 300 python -u bench.py > $out/bench.json 2> $out/bench.err
+out=gpurun_out/ab23; mkdir -p $out
+E=$PWD/tfg---quantum-byzantine-agreement_amd/_build/exp
+QBA_LIB=$E/b_fused2.so timeout -k 10 120 python tools/exp/parity11.py > $out/parity_b_fused2.txt 2>&1
+ROUNDS=2 timeout -k 10 600 bash tools/exp/ab_c1.sh ab23c1
