@@ -1,5 +1,5 @@
 set -eo pipefail
-out=gpurun_out/ab23; mkdir -p $out
+out=gpurun_out/ab24; mkdir -p $out
 E=$PWD/tfg---quantum-byzantine-agreement_amd/_build/exp
-QBA_LIB=$E/b_fused2.so timeout -k 10 120 python tools/exp/parity11.py > $out/parity_b_fused2.txt 2>&1
-ROUNDS=2 timeout -k 10 600 bash tools/exp/ab_c1.sh ab23c1
+QBA_LIB=$E/b_r16.so timeout -k 10 120 python tools/exp/parity11.py > $out/parity_b_r16.txt 2>&1
+ROUNDS=3 timeout -k 10 900 bash tools/exp/ab_c1.sh ab24c1
