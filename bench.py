@@ -484,10 +484,11 @@ def full_circuit_n7(eng, n=7):
 
 def main():
     args = parse()
-    # The headline's first ~40 launches after the GPU idles run 400-520 us and
-    # then settle at ~366 us for as long as the launches continue (per-launch
-    # kernel trace over 2050 launches: profiles/r1/launch_drift.txt), so its
-    # default window is 50 untimed + 200 timed launches (~0.1 s in total).
+    # After the GPU idles the headline's launches dip to ~450 us (the clock
+    # drops to ~1.9 GHz at launches 6-12) and settle at ~316 us after ~100
+    # launches (per-launch trace: profiles/r2/drift_fused_final.txt), so its
+    # default window is 50 untimed + 200 timed launches (~0.1 s in total);
+    # the driver's own --steps 20 --warmup 5 window is reported as given.
     # configs[1] and [3] run the same kernels, so they get the same window
     long_window = args.config in (1, 2, 3)
     if args.steps is None:
