@@ -120,6 +120,9 @@ static void check_circuits(std::mt19937_64 &rng) {
     const QbaProgramSet *ps = reinterpret_cast<const QbaProgramSet *>(img.data());
     CHECK(ps->canonical == 1, "canonical flag n=%d", n);
     CHECK(ps->closed == (n <= QBA_CLOSED_MAX_N ? 1 : 0), "closed flag n=%d", n);
+    if (ps->closed)  // the list kernels stage the tables with 16-B loads of whole 16-B words
+      CHECK(ps->perm_off % 16 == 0 && img.size() >= (size_t)ps->perm_off + 16 * (((size_t)ps->perm_words + 3) / 4),
+            "stage tables not 16-B aligned / padded n=%d", n);
     // malformed circuits
     std::vector<int32_t> bad = q_gates(n, perm), kept;
     if (n >= 2) {
