@@ -481,7 +481,11 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
       const int g = 4 * i + b;
       if (g < C::G && g != 1) {  // H[u][1][x] = [x == u] |P_u|, derived when reduced
         const uint32_t a = qba_add_byte(hb, E, b);
+#ifdef QBA_EXP_NOATOMIC  // experiment builds: the address work without the LDS atomic
+        asm volatile("" ::"v"(a));
+#else
         atomicAdd((uint32_t *)((qba_lds_u32 *)(uintptr_t)a + g * C::WP), 1u);
+#endif
       }
     }
   }

@@ -1,2 +1,2 @@
 set -eo pipefail
-bash tools/rehearse_world2.sh
+ROUNDS=1 timeout -k 10 1100 bash tools/exp/ab.sh ab26
