@@ -5,8 +5,11 @@
 // (tfg.py:182) and the support of a statevector (resource compilation).
 // Three launches: per-tile counts, a single-workgroup exclusive scan of the
 // tile counts, and an emit pass that re-evaluates the predicate and writes
-// each selected item at its global rank.  A tile is 256 threads x 16 items;
-// each thread owns 16 consecutive items.
+// each selected item at its global rank.  A tile is 256 threads x 16 items.
+// The predicate is evaluated coalesced (round r: thread t tests item
+// r * 256 + t of the tile, so a wave reads 64 consecutive items); the emit
+// pass stages the flags in LDS and ranks them with each thread owning 16
+// consecutive items.
 #pragma once
 
 #include "qba_internal.h"
@@ -19,11 +22,11 @@ template <class Pred>
 __global__ void __launch_bounds__(QBA_CT_THREADS)
     qba_k_compact_count(Pred p, int64_t n, int32_t *__restrict__ tile_counts) {
   __shared__ int32_t wsum[QBA_CT_THREADS / 64];
-  const int64_t tile = blockIdx.x;
-  const int64_t base = tile * QBA_CT_TILE + (int64_t)threadIdx.x * QBA_CT_ITEMS;
+  const int64_t tbase = (int64_t)blockIdx.x * QBA_CT_TILE;
   int32_t c = 0;
-  for (int k = 0; k < QBA_CT_ITEMS; ++k) {
-    const int64_t i = base + k;
+#pragma unroll
+  for (int r = 0; r < QBA_CT_ITEMS; ++r) {
+    const int64_t i = tbase + r * QBA_CT_THREADS + threadIdx.x;
     if (i < n && p.test(i)) ++c;
   }
   for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
@@ -32,7 +35,7 @@ __global__ void __launch_bounds__(QBA_CT_THREADS)
   if (threadIdx.x == 0) {
     int32_t s = 0;
     for (int w = 0; w < QBA_CT_THREADS / 64; ++w) s += wsum[w];
-    tile_counts[tile] = s;
+    tile_counts[blockIdx.x] = s;
   }
 }
 
@@ -45,13 +48,22 @@ template <class Pred>
 __global__ void __launch_bounds__(QBA_CT_THREADS)
     qba_k_compact_emit(Pred p, int64_t n, const int64_t *__restrict__ offsets, int64_t cap) {
   __shared__ int32_t wsum[QBA_CT_THREADS / 64];
+  __shared__ uint32_t flags[QBA_CT_TILE / 4];  // one byte per item of the tile
   const int64_t tile = blockIdx.x;
-  const int64_t base = tile * QBA_CT_TILE + (int64_t)threadIdx.x * QBA_CT_ITEMS;
-  uint32_t bits = 0;
-  for (int k = 0; k < QBA_CT_ITEMS; ++k) {
-    const int64_t i = base + k;
-    if (i < n && p.test(i)) bits |= 1u << k;
+  const int64_t tbase = tile * QBA_CT_TILE;
+  uint8_t *f8 = reinterpret_cast<uint8_t *>(flags);
+#pragma unroll
+  for (int r = 0; r < QBA_CT_ITEMS; ++r) {
+    const int64_t i = tbase + r * QBA_CT_THREADS + threadIdx.x;
+    f8[r * QBA_CT_THREADS + threadIdx.x] = (i < n && p.test(i)) ? 1 : 0;
   }
+  __syncthreads();
+  // this thread's 16 consecutive items: 4 flag words, 0/1 bytes -> 4 bits each
+  const int64_t base = tbase + (int64_t)threadIdx.x * QBA_CT_ITEMS;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int q = 0; q < QBA_CT_ITEMS / 4; ++q)
+    bits |= ((flags[threadIdx.x * (QBA_CT_ITEMS / 4) + q] * 0x01020408u) >> 24) << (4 * q);
   const int32_t c = __popc(bits);
   // inclusive scan over the wave
   int32_t incl = c;
