@@ -343,6 +343,24 @@ def test_ghz_register_statevector(engine):
     assert np.max(np.abs(prob - 0.5)) < 1e-12
 
 
+def test_compaction_multiblock_scan(engine):
+    """isQCorrList over more than 8192 tiles of 4096 entries: the tile counts
+    are scanned by the three-launch path (block sums, their scan, block
+    scans); the ascending index list must equal numpy's, including a ragged
+    last tile and runs of empty tiles."""
+    rng = np.random.default_rng(11)
+    count = 8192 * 4096 + 3 * 4096 + 777
+    l0 = rng.integers(0, 4, count, dtype=np.uint8)
+    l1 = l0.copy()
+    flip = rng.random(count) < 0.3
+    flip[5_000_000:9_000_000] = False          # empty tiles
+    flip[20_000_000:20_100_000] = True         # full tiles
+    l1[flip] ^= 1
+    want = np.nonzero(l0 != l1)[0]
+    got = engine.isq_indices(engine.to_device(l0), engine.to_device(l1))
+    assert got.shape == want.shape and np.array_equal(got, want)
+
+
 def test_exact_mode_kernels(engine):
     rng = np.random.default_rng(3)
     for count in (1, 17, 1000, 70_001):

@@ -44,6 +44,16 @@ __global__ void __launch_bounds__(1024)
     qba_k_compact_scan(const int32_t *__restrict__ counts, int64_t ntiles,
                        int64_t *__restrict__ offsets, int64_t *__restrict__ total);
 
+// multi-block scan of large tile-count arrays (qba_exact.hip)
+#define QBA_SC_T 1024
+#define QBA_SC_PER 8
+#define QBA_SC_CH (QBA_SC_T * QBA_SC_PER)
+__global__ void __launch_bounds__(QBA_SC_T)
+    qba_k_scan_reduce(const int32_t *__restrict__ counts, int64_t ntiles, int32_t *__restrict__ bsum);
+__global__ void __launch_bounds__(QBA_SC_T)
+    qba_k_scan_apply(const int32_t *__restrict__ counts, int64_t ntiles, const int64_t *__restrict__ boff,
+                     int64_t *__restrict__ offsets);
+
 template <class Pred>
 __global__ void __launch_bounds__(QBA_CT_THREADS)
     qba_k_compact_emit(Pred p, int64_t n, const int64_t *__restrict__ offsets, int64_t cap) {
@@ -94,17 +104,29 @@ static int qba_compact(qba_ctx *ctx, Pred p, int64_t n, int64_t cap, int64_t *co
     return QBA_OK;
   }
   const int64_t ntiles = (n + QBA_CT_TILE - 1) / QBA_CT_TILE;
-  const size_t need = ntiles * sizeof(int32_t) + ntiles * sizeof(int64_t) + 64;
+  const int64_t nb = (ntiles + QBA_SC_CH - 1) / QBA_SC_CH;  // scan blocks (large inputs)
+  // [offsets int64 ntiles | block offsets int64 nb | counts int32 ntiles (16-B aligned) | block sums int32 nb]
+  const int64_t n64 = (ntiles + nb + 1) & ~(int64_t)1;  // counts start 16-B aligned (int4 loads)
+  const size_t need = n64 * sizeof(int64_t) + ((ntiles + 3) & ~3) * sizeof(int32_t) + nb * sizeof(int32_t) + 64;
   int rc = qba_ensure_scan(ctx, need);
   if (rc) return rc;
   int64_t *offsets = reinterpret_cast<int64_t *>(ctx->scan);
-  int32_t *counts = reinterpret_cast<int32_t *>(offsets + ntiles);
+  int64_t *boff = offsets + ntiles;
+  int32_t *counts = reinterpret_cast<int32_t *>(offsets + n64);
+  int32_t *bsum = counts + ((ntiles + 3) & ~3);
   if (ntiles > 0x7fffffffLL) return qba_fail(QBA_EUNSUPPORTED, "compaction: input too large");
   hipLaunchKernelGGL(qba_k_compact_count<Pred>, dim3((unsigned)ntiles), dim3(QBA_CT_THREADS), 0,
                      stream, p, n, counts);
   QBA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(qba_k_compact_scan, dim3(1), dim3(1024), 0, stream, counts, ntiles, offsets,
-                     ctx->count1);
+  if (nb <= 1) {
+    hipLaunchKernelGGL(qba_k_compact_scan, dim3(1), dim3(1024), 0, stream, counts, ntiles, offsets,
+                       ctx->count1);
+  } else {
+    hipLaunchKernelGGL(qba_k_scan_reduce, dim3((unsigned)nb), dim3(QBA_SC_T), 0, stream, counts, ntiles, bsum);
+    hipLaunchKernelGGL(qba_k_compact_scan, dim3(1), dim3(1024), 0, stream, bsum, nb, boff, ctx->count1);
+    hipLaunchKernelGGL(qba_k_scan_apply, dim3((unsigned)nb), dim3(QBA_SC_T), 0, stream, counts, ntiles, boff,
+                       offsets);
+  }
   QBA_HIP(hipGetLastError());
   hipLaunchKernelGGL(qba_k_compact_emit<Pred>, dim3((unsigned)ntiles), dim3(QBA_CT_THREADS), 0,
                      stream, p, n, offsets, cap);

@@ -34,6 +34,76 @@ __global__ void __launch_bounds__(1024)
   if (t == 1023) *total = part[1023];
 }
 
+// Exclusive scan of a large tile-count array in three launches: per-block
+// sums of QBA_SC_CH counts (each thread 8 consecutive counts, 16-B loads),
+// the single-workgroup scan above over the block sums, then each block's
+// scan with its offset added.  The single-workgroup scan alone walks its
+// per-thread chunks serially: 8.4 M tile counts (a 35-qubit support) took
+// ~15 ms that way.
+__device__ __forceinline__ int64_t qba_block_exscan(int64_t v, int64_t *wtot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wtot[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t run = 0;
+    for (int k = 0; k < QBA_SC_T / 64; ++k) {
+      const int64_t t = wtot[k];
+      wtot[k] = run;
+      run += t;
+    }
+    wtot[QBA_SC_T / 64] = run;
+  }
+  __syncthreads();
+  return wtot[w] + incl - v;
+}
+
+__device__ __forceinline__ void qba_sc_load(const int32_t *__restrict__ counts, int64_t ntiles, int32_t (&c)[QBA_SC_PER]) {
+  const int64_t i0 = (int64_t)blockIdx.x * QBA_SC_CH + (int64_t)threadIdx.x * QBA_SC_PER;
+  if (i0 + QBA_SC_PER <= ntiles) {
+    const int4 a = reinterpret_cast<const int4 *>(counts + i0)[0], b = reinterpret_cast<const int4 *>(counts + i0)[1];
+    c[0] = a.x, c[1] = a.y, c[2] = a.z, c[3] = a.w, c[4] = b.x, c[5] = b.y, c[6] = b.z, c[7] = b.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < QBA_SC_PER; ++k) c[k] = i0 + k < ntiles ? counts[i0 + k] : 0;
+  }
+}
+
+__global__ void __launch_bounds__(QBA_SC_T)
+    qba_k_scan_reduce(const int32_t *__restrict__ counts, int64_t ntiles, int32_t *__restrict__ bsum) {
+  __shared__ int64_t wtot[QBA_SC_T / 64 + 1];
+  int32_t c[QBA_SC_PER];
+  qba_sc_load(counts, ntiles, c);
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < QBA_SC_PER; ++k) s += c[k];
+  qba_block_exscan(s, wtot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = (int32_t)wtot[QBA_SC_T / 64];  // < 2^31: 8192 tiles x 4096 items
+}
+
+__global__ void __launch_bounds__(QBA_SC_T)
+    qba_k_scan_apply(const int32_t *__restrict__ counts, int64_t ntiles, const int64_t *__restrict__ boff,
+                     int64_t *__restrict__ offsets) {
+  __shared__ int64_t wtot[QBA_SC_T / 64 + 1];
+  int32_t c[QBA_SC_PER];
+  qba_sc_load(counts, ntiles, c);
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < QBA_SC_PER; ++k) s += c[k];
+  int64_t run = boff[blockIdx.x] + qba_block_exscan(s, wtot);
+  const int64_t i0 = (int64_t)blockIdx.x * QBA_SC_CH + (int64_t)threadIdx.x * QBA_SC_PER;
+#pragma unroll
+  for (int k = 0; k < QBA_SC_PER; ++k) {
+    if (i0 + k < ntiles) offsets[i0 + k] = run;
+    run += c[k];
+  }
+}
+
 // --- isQCorrList = {k : Li[k] != Lc[k]}  (tfg.py:327) -------------------------------
 struct QbaIsqPred {
   const uint8_t *l0, *l1;
