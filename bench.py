@@ -4,6 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
+`python bench.py --gpus N` outside torchrun launches the N ranks itself (one
+process per GPU under torch.distributed.run, see launch_ranks) and prints rank
+0's line, so both forms measure the same thing.
+
 One step (default, --config 2) = one pass of the hot path over this rank's
 shard of sizeL: every entry is Born-sampled from the compiled resource program
 (Philox keyed by the global entry index), its n+1 list bytes are written to
@@ -482,8 +486,53 @@ def full_circuit_n7(eng, n=7):
     return out
 
 
+def launch_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` with no WORLD_SIZE in the environment: start
+    the N ranks ourselves, exactly as the driver's torchrun line would (one
+    process per GPU, rendezvous on 127.0.0.1), and relay rank 0's JSON line.
+
+    This process never touches the GPU (no torch import): the ranks are
+    children started with subprocess, not an exec of this process.
+    QBA_BENCH_WORKER names another script to launch in place of this one (the
+    CPU test of the launcher); QBA_BENCH_LAUNCH_TIMEOUT bounds the whole run."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = os.environ.get("QBA_BENCH_WORKER") or str(Path(__file__).resolve())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", script, *argv]
+    timeout = float(os.environ.get("QBA_BENCH_LAUNCH_TIMEOUT", "1500"))
+    # stdout is relayed line by line (the driver reads the one JSON line),
+    # stderr passes straight through
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, _ = proc.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        import signal
+        os.killpg(proc.pid, signal.SIGKILL)  # the launcher's own process group only
+        proc.communicate()
+        print(f"bench.py: {n}-rank launch exceeded {timeout:.0f} s", file=sys.stderr)
+        return 124
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    for ln in out.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if proc.returncode == 0 and len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    for ln in lines:
+        print(ln, flush=True)
+    return proc.returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.config != 2:
+            raise SystemExit("--config 0/1/3/4 are single-GPU measurements")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     # After the GPU idles the headline's launches dip to ~450 us (the clock
     # drops to ~1.9 GHz at launches 6-12) and settle at ~316 us after ~100
     # launches (per-launch trace: profiles/r2/drift_fused_final.txt), so its

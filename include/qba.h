@@ -64,6 +64,10 @@ enum { QBA_GATE_H = 0, QBA_GATE_X = 1 }; /* gate triples: {kind, target, control
 /* ---- library / context ---------------------------------------------------------- */
 QBA_API const char *qba_last_error(void);
 QBA_API int qba_version(void); /* major*10000 + minor*100 + patch */
+/* Nonzero when any object of this library was compiled with an experiment
+ * switch (tools/exp/build.sh A/B builds, some wrong by design); 0 for the
+ * shipped build. */
+QBA_API int qba_build_flags(void);
 QBA_API int qba_init(int device, qba_ctx **out);
 QBA_API int qba_destroy(qba_ctx *ctx);
 /* Pre-allocate scratch for counts launches of up to `max_blocks` workgroups so

@@ -48,3 +48,20 @@ def test_countmode_sampled_honest_run(engine):
     run = protocol.run_local(11, 2_000_000, 0, engine, seed=4, party_cls=countmode.CountParty)
     assert run.result["success"] and run.error is None
     assert len(set(run.result["decisions"])) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [4, 9, 23])
+def test_countmode_config1_matches_c_twin(engine, seed):
+    """BASELINE configs[1] as stated: n = 11, 3 dishonest, sizeL = 1e6 of
+    device-sampled lists.  The whole count-mode run on the GPU engine equals
+    the same run whose count tables come from the C twin (oracle, same
+    Philox schedule): decisions, dishonest ids, V_i, accept / reject / sent
+    of every rank."""
+    protocol, countmode = sub("protocol"), sub("countmode")
+    kw = dict(seed=seed, timeout=120, party_cls=countmode.CountParty)
+    got = protocol.run_local(11, 1_000_000, 3, engine, **kw)
+    want = protocol.run_local(11, 1_000_000, 3, OracleEngine(), **kw)
+    assert len(got.result["dishonest"]) == 3
+    assert got.result == want.result and got.V == want.V and got.error_ranks == want.error_ranks
+    assert got.accept == want.accept and got.reject == want.reject and got.sent == want.sent

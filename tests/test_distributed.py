@@ -92,7 +92,7 @@ def test_sharded_counts_allreduce_gloo(world):
             assert np.array_equal(got, whole * (k + 1)), k
 
 
-def _countparty_worker(rank, world, port, spec, out_q):
+def _countparty_worker(rank, world, port, spec, out_q, hip=False):
     """Torch rank `rank` of a world of GPU owners (gloo here): rank 0 hosts the
     whole count-mode protocol (LocalWorld threads) and its QSD's count pass
     is the sharded ShardCounter; the other ranks only compute their shard and
@@ -111,7 +111,9 @@ def _countparty_worker(rank, world, port, spec, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     d.init("gloo")
-    eng = OracleEngine()
+    # hip: every rank's shard is sampled and checked by the HIP engine on
+    # device 0 (a one-GPU rehearsal of the GPU-owner layout), reduced over gloo
+    eng = importlib.import_module(f"{pkg}.engine").Engine(0) if hip else OracleEngine()
     counter = countmode.ShardCounter(eng, rank, world, countmode.torch_allreduce, owners={0})
     n, sizeL, ndis, seed, lists = spec
     if rank == 0:
@@ -127,11 +129,11 @@ def _countparty_worker(rank, world, port, spec, out_q):
     dist.destroy_process_group()
 
 
-def _run_world(spec, world=2):
+def _run_world(spec, world=2, hip=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_countparty_worker, args=(r, world, port, spec, q)) for r in range(world)]
+    procs = [ctx.Process(target=_countparty_worker, args=(r, world, port, spec, q, hip)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=180)
@@ -167,4 +169,20 @@ def test_countparty_sharded_sampled_equals_unsharded():
     one = protocol.run_local(n, sizeL, ndis, OracleEngine(), seed=seed, timeout=60, party_cls=countmode.CountParty)
     got = _run_world((n, sizeL, ndis, seed, None))
     assert got["decisions"] == one.result["decisions"] and got["success"] == one.result["success"]
+    assert got["accept"] == one.accept and got["reject"] == one.reject and got["sent"] == one.sent
+
+
+@pytest.mark.gpu
+def test_countparty_sharded_hip_engine_equals_unsharded(engine):
+    """The sharded count pass with the HIP engine (not the numpy oracle):
+    two torch ranks on device 0, each samples + checks its half of sizeL on
+    the GPU, one gloo all-reduce; the protocol decides exactly like the
+    one-process GPU run (BASELINE configs[1]: n = 11, 3 dishonest, 1e6)."""
+    protocol, countmode = sub("protocol"), sub("countmode")
+    n, sizeL, ndis, seed = 11, 1_000_001, 3, 7
+    one = protocol.run_local(n, sizeL, ndis, engine, seed=seed, timeout=60, party_cls=countmode.CountParty)
+    got = _run_world((n, sizeL, ndis, seed, None), hip=True)
+    assert got["decisions"] == one.result["decisions"] and got["success"] == one.result["success"]
+    assert got["dishonest"] == one.result["dishonest"]
+    assert got["V"] == {str(k): v for k, v in one.V.items()}
     assert got["accept"] == one.accept and got["reject"] == one.reject and got["sent"] == one.sent

@@ -167,6 +167,20 @@ def test_library_exports_every_declared_symbol():
     assert lib.qba_version() >= 100
 
 
+def test_shipped_library_has_no_experiment_switch():
+    """The libqba.so in the tree (the one the GPU tests, smoke and bench load)
+    carries no QBA_EXP_* / tuning override: qba_build_flags() is 0, and a
+    build that sets a switch without QBA_EXPERIMENT_BUILD fails to compile."""
+    import subprocess
+    lib = sub("_lib").lib()
+    assert lib.qba_build_flags() == 0
+    csrc = ROOT / "tfg---quantum-byzantine-agreement_amd" / "csrc"
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "--offload-arch=gfx950", "-fsyntax-only",
+                        "-DQBA_EXP_NOTABLE", "-x", "hip", str(csrc / "qba_ctx.hip")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "QBA_EXPERIMENT_BUILD" in r.stderr
+
+
 def test_library_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():
@@ -199,7 +213,7 @@ import ctypes as C, importlib, json, sys
 sys.path.insert(0, sys.argv[1])
 lm = importlib.import_module("tfg---quantum-byzantine-agreement_amd._lib")
 lib = lm.lib()
-skip = {"qba_last_error", "qba_version", "qba_destroy", "qba_rccl_unique_id"}
+skip = {"qba_last_error", "qba_version", "qba_build_flags", "qba_destroy", "qba_rccl_unique_id"}
 out = {}
 for name, argt in sorted(lm.SIGNATURES.items()):
     if name in skip:

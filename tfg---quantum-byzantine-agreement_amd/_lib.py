@@ -28,6 +28,7 @@ _pi32, _pi64, _pu64, _pf64 = C.POINTER(_i32), C.POINTER(_i64), C.POINTER(_u64), 
 SIGNATURES = {
     "qba_last_error": [],
     "qba_version": [],
+    "qba_build_flags": [],
     "qba_init": [C.c_int, C.POINTER(_p)],
     "qba_destroy": [_p],
     "qba_reserve": [_p, C.c_int, _i64],

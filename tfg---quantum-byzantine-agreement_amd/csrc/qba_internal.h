@@ -13,6 +13,28 @@
 
 #include "../../include/qba.h"
 
+// ---------------------------------------------------------------------------
+// Experiment switches (tools/exp/build.sh) exist only for A/B builds; several
+// make the results wrong by design.  A build that sets any of them must also
+// define QBA_EXPERIMENT_BUILD, so the shipped libqba.so cannot carry one, and
+// qba_build_flags() reports which were compiled in (0 for a shipped build;
+// tests/test_oracle_golden.py asserts it).
+// ---------------------------------------------------------------------------
+#if defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||            \
+    defined(QBA_EXP_NOTABLE) || defined(QBA_EXP_CHEAPRNG) || defined(QBA_EXP_NOATOMIC) ||          \
+    defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_INTERLEAVE) ||             \
+    defined(QBA_EXP_GRID) || defined(QBA_EXP_NARROW) || defined(QBA_WIDE_QPT) || defined(QBA_MINW) || \
+    defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) || defined(QBA_RED_ALL_IN_FLIGHT) ||           \
+    defined(QBA_QUEUE) || defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || \
+    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N)
+#ifndef QBA_EXPERIMENT_BUILD
+#error "an experiment switch is set without QBA_EXPERIMENT_BUILD (tools/exp/build.sh): not a shippable libqba"
+#endif
+#define QBA_BUILD_EXPERIMENT_FLAGS 1
+#else
+#define QBA_BUILD_EXPERIMENT_FLAGS 0
+#endif
+
 #define QBA_MAX_FACTORS 16
 #define QBA_MAX_TABLE 4096   // uint64 table entries per kind (LDS budget)
 #define QBA_BLOCK 256        // threads per workgroup (batched / helper kernels)

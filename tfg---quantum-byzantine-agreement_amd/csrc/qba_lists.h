@@ -34,3 +34,6 @@ template <int NP>
 int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L);
 template <int NP>
 int qba_launch_batched(qba_ctx *ctx, const QbaBatch &B);
+// QBA_BUILD_EXPERIMENT_FLAGS of the per-n object (qba_build_flags ORs them)
+template <int NP>
+int qba_lists_build_flags();

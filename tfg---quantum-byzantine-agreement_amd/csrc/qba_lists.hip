@@ -7,6 +7,18 @@
 #define QBA_ONLY_N 0
 #endif
 
+// 0 for a shipped build: no experiment switch in this object or in any
+// per-n list-kernel object linked with it (qba_internal.h)
+extern "C" int qba_build_flags(void) {
+  int f = QBA_BUILD_EXPERIMENT_FLAGS;
+#define QBA_FLAG(k) \
+  if constexpr (QBA_ONLY_N == 0 || k == QBA_ONLY_N) f |= qba_lists_build_flags<k>();
+  QBA_FLAG(1) QBA_FLAG(2) QBA_FLAG(3) QBA_FLAG(4) QBA_FLAG(5) QBA_FLAG(6) QBA_FLAG(7) QBA_FLAG(8)
+  QBA_FLAG(9) QBA_FLAG(10) QBA_FLAG(11) QBA_FLAG(12) QBA_FLAG(13) QBA_FLAG(14) QBA_FLAG(15)
+#undef QBA_FLAG
+  return f;
+}
+
 static int nbins_of(int n) {  // QCfg<n>::NBP
   const int g = n + 1, q = qba_nq(n), w = 1 << q;
   return (w * g * (w + 1) + w * g * (g - 1) / 2 + 2 + 3) & ~3;

@@ -8,3 +8,4 @@
 
 template int qba_launch_lists<QBA_INST_N>(qba_ctx *ctx, const QbaLaunch &L);
 template int qba_launch_batched<QBA_INST_N>(qba_ctx *ctx, const QbaBatch &B);
+template <> int qba_lists_build_flags<QBA_INST_N>() { return QBA_BUILD_EXPERIMENT_FLAGS; }

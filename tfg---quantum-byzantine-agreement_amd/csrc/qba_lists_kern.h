@@ -470,9 +470,15 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
     return;
   }
   // hoff: the histogram's LDS byte address held in a VGPR by the caller (the
-  // row base is then one v_mad_u32_u24 with the stride in an SGPR)
+  // row base is then one v_mad_u32_u24 with the stride in an SGPR).  The row
+  // index is taken to nq bits (the same single v_bfe): a trusted value is
+  // < W already, and whatever the bytes hold the address stays inside this
+  // workgroup's histogram + queue area (x < 256 adds at most 1 KiB).  An
+  // experiment build that fed unmasked words here once indexed rows up to
+  // 255 * 816 B past the histogram, beyond the LDS allocation, and faulted.
+  const uint32_t l1r = (D[0] >> 8) & (uint32_t)(C::W - 1);
   if (hoff == 0xffffffffu) hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
-  const uint32_t hb = hoff + l1 * (uint32_t)(C::G * C::WP * 4);
+  const uint32_t hb = hoff + l1r * (uint32_t)(C::G * C::WP * 4);
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) {
     const uint32_t E = D[i] << 2;  // byte b = 4 * value (< 64: no carry into the next byte)
@@ -506,7 +512,7 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
   if (__popc(U) != C::G) {  // some pair collides: exact slow path
     // a compact loop (values picked by selects, no private array): this
     // path is rare and unrolling it would multiply the kernel's code size
-    uint32_t *c = hist + C::HBL + l1 * C::CP;
+    uint32_t *c = hist + C::HBL + l1r * C::CP;
     const uint32_t w0 = D[0], w1 = F::ND > 1 ? D[F::ND > 1 ? 1 : 0] : 0u,
                    w2 = F::ND > 2 ? D[F::ND > 2 ? 2 : 0] : 0u, w3 = F::ND > 3 ? D[F::ND > 3 ? 3 : 0] : 0u;
     int pi = 0;
