@@ -106,6 +106,34 @@ def cpu_baseline_counts(n, seed, info, target_s):
                       f"(oracle/sampler_ref.c) sample + count, {dt:.1f} s"}
 
 
+def cpu_baseline_mpiexec(runs):
+    """BASELINE.md CPU plan item 2: the Python restatement of tfg.py under a
+    real `mpiexec -n 4` at configs[0] (tests/mpi_cpu_baseline.py: the
+    package's protocol host, one process per party, numpy engine on the host
+    cores).  Reports the protocol wall per run (max over ranks) and the whole
+    command's wall, start-up included (as `time mpiexec -n 4 python tfg.py
+    1000 1` would).  None when no mpiexec is installed."""
+    import shutil
+    import subprocess
+    mpiexec = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
+    if not os.path.exists(mpiexec):
+        return None
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("PMI_", "OMPI_"))}
+    t0 = time.perf_counter()
+    p = subprocess.run([mpiexec, "-n", "4", sys.executable, str(ROOT / "tests" / "mpi_cpu_baseline.py"),
+                        "--runs", str(runs)], capture_output=True, text=True, timeout=300, env=env)
+    wall = time.perf_counter() - t0
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode or not lines:
+        return {"error": (p.stderr or p.stdout)[-300:]}
+    r = json.loads(lines[-1])
+    return {"value": r["entries_per_s"], "unit": "entries/s (protocol run, sizeL=1000)", "cores": 4,
+            "kind": "port", "ms_per_run": r["ms_per_run_median"], "command_wall_s": wall,
+            "sample": f"mpiexec -n 4: {runs} protocol runs of n=3, 1 dishonest, sizeL=1000 (+1 warm-up), the "
+                      "package's host with the numpy engine on the host CPU, one process per party "
+                      "(tests/mpi_cpu_baseline.py); command_wall_s includes MPI and Python start-up"}
+
+
 def _lib_sha16():
     """sha256 (16 hex) of the libqba.so this process loads (PMC figures are per build)."""
     import hashlib
@@ -305,6 +333,9 @@ def config0(args, eng):
         extra["cpu_baseline"] = {"value": 1000 / cdt, "unit": "entries/s", "cores": 1, "kind": "port",
                                  "sample": f"{args.steps} protocol runs, numpy oracle engine in place of "
                                            f"the GPU engine (lists drawn on the host)"}
+        mpi_leg = cpu_baseline_mpiexec(max(args.steps, 10))
+        if mpi_leg is not None:
+            extra["cpu_baseline_mpiexec"] = mpi_leg
     return _line(args, 1000 / dt, "entries/s (whole protocol run, sizeL=1000)",
                  "BASELINE configs[0]: n=3 parties, 1 dishonest, sizeL=1000, protocol rounds "
                  "(in-process mpiexec world)",

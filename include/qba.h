@@ -203,6 +203,15 @@ QBA_API int qba_check_packet_host(qba_ctx *ctx, const uint8_t *li_dev, uint64_t 
                                   const int64_t *stage_host, int64_t m, int64_t len, int64_t v, int64_t w,
                                   int64_t *out_host, qba_stream stream);
 
+/* A whole round of received packets (tfg.py:337-348 -> 289-294) in ONE host
+ * round trip: k stages concatenated in stage_host (packet i: len_i*(m_i+1)
+ * int64 = [order | rows], desc[i] = {m_i, len_i, v_i}); out_host receives the
+ * k outputs concatenated (packet i: len_i + 3 + m_i int64, as
+ * qba_check_packet).  One H2D, k launches, one D2H, one sync. */
+QBA_API int qba_check_packets_host(qba_ctx *ctx, const uint8_t *li_dev, uint64_t list_len,
+                                   const int64_t *stage_host, const int64_t *desc, int64_t k, int64_t w,
+                                   int64_t *out_host, qba_stream stream);
+
 /* ---- wire-compatible codec (rawS layout, tfg.py:81-84, 128-129, 142-161) -------- */
 QBA_API int qba_bits_to_values(qba_ctx *ctx, const int64_t *raw_dev, uint64_t count, int nq,
                        uint8_t *values_dev, qba_stream stream);

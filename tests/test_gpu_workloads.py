@@ -125,6 +125,27 @@ def test_chunk_crossing_2p31(engine):
     assert np.array_equal(flat[h + cc:], P)
 
 
+@pytest.mark.parametrize("col", [0, 4])
+def test_phi_span_crossing_unaligned_first(engine, col):
+    """One call across a multiple of 2^33 entries (the launch split that keeps
+    the Philox counter's high word uniform) with first % 8 != 0, into rows
+    whose first column is 8-B aligned (col 0) or only 4-B aligned (col 4):
+    the alignment chunks keep the later launches on the wide kernel and the
+    lists / counts stay bit-exact against the C twin."""
+    n, seed = 11, 0x5EED
+    first, count = (1 << 33) - 1_000_003, 2_000_013
+    info = engine.prepare(n)
+    buf = engine.alloc_lists(n, count + 8)
+    lists = buf[:, col:]
+    _, c = engine.sample_check(n, seed, first, count, lists)
+    torch.cuda.synchronize()
+    ref = oracle_lib.sample(n, seed, first, count, info["notq"], info["q"], info["closed"])
+    assert np.array_equal(lists[:, :count].cpu().numpy(), ref)
+    H, C, P, bad = oracle_lib.counts(ref, n)
+    assert bad == 0
+    _assert_counts(c, H, C, P, f"2^33 crossing, column {col}")
+
+
 def test_config3_full_batched(engine):
     """BASELINE configs[3]: 4096 independent 7-party instances x sizeL = 1e5
     per GPU; every instance's counts vs the C twin, 16 instances' lists."""

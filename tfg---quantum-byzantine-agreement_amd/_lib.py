@@ -50,6 +50,7 @@ SIGNATURES = {
     "qba_check_gather": [_p, _p, C.c_uint64, C.c_int, C.c_uint64, _p, _p, _i64, _i64, _i64, _i64, _p, _p],
     "qba_check_packet": [_p, _p, _u64, _p, _i64, _i64, _i64, _i64, _p, _p],
     "qba_check_packet_host": [_p, _p, _u64, _p, _i64, _i64, _i64, _i64, _p, _p],
+    "qba_check_packets_host": [_p, _p, _u64, _p, _p, _i64, _i64, _p, _p],
     "qba_lists_to_bits_host": [_p, _p, _u64, C.c_int, _u64, C.c_int, _p, _p],
     "qba_bits_to_values_host": [_p, _p, _u64, C.c_int, _p, _p],
     "qba_rccl_unique_id": [_p],

@@ -510,3 +510,6 @@ class EpochComm:
     def Barrier(self) -> None:
         self.inner.Barrier()
         self.epoch += 1
+        # a probe's epoch only names the packet it found; after the barrier
+        # every explicit-tag receive uses this rank's own epoch again
+        self._probed.clear()

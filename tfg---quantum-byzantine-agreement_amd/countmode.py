@@ -101,14 +101,41 @@ class ShardCounter:
         return party_rank in self._owners if self._owners is not None else party_rank < self.world
 
     def tables(self, n: int, sizeL: int, seed: int, lists=None) -> np.ndarray:
-        from .distributed import shard_bounds
+        """Sum of every owner's [H | C | P]; raises on EVERY owner when any
+        owner's count pass failed.  The buffer carries one extra int64, the
+        number of owners that failed: an owner whose pass raised still joins
+        the collective (with zero tables and its flag set), so no rank is
+        left blocked in the all-reduce."""
+        from .distributed import count_layout, shard_bounds
         first, count = shard_bounds(sizeL, self.rank, self.world)
-        if lists is not None:
-            part = np.ascontiguousarray(np.asarray(lists)[:, first:first + count])
-            flat = self.engine.count_tables(n, count, seed, lists=part, device_out=True)
-        else:
-            flat = self.engine.count_tables(n, count, seed, first=first, device_out=True)
-        return np.asarray(self.allreduce(flat))
+        err = None
+        try:
+            if lists is not None:
+                part = np.ascontiguousarray(np.asarray(lists)[:, first:first + count])
+                flat = self.engine.count_tables(n, count, seed, lists=part, device_out=True)
+            else:
+                flat = self.engine.count_tables(n, count, seed, first=first, device_out=True)
+        except Exception as e:  # noqa: BLE001 -- re-raised below, after the collective
+            err, flat = e, None
+        out = np.asarray(self.allreduce(self._flagged(flat, err is not None, count_layout(n)[3])))
+        if out[-1] != 0:
+            if err is not None:
+                raise err
+            from ._lib import QbaError
+            raise QbaError(f"count pass failed on {int(out[-1])} of {self.world} shard owner(s)")
+        return out[:-1]
+
+    def _flagged(self, flat, failed: bool, size: int):
+        """[flat | failed] in the form the all-reduce takes (device tensor for
+        a GPU engine, host array otherwise); zero tables when the pass failed."""
+        import torch
+        dev = getattr(self.engine, "device", None)
+        if isinstance(flat, torch.Tensor) or (flat is None and dev is not None):
+            dev = flat.device if isinstance(flat, torch.Tensor) else dev
+            body = flat if flat is not None else torch.zeros(size, dtype=torch.int64, device=dev)
+            return torch.cat([body, torch.tensor([int(failed)], dtype=torch.int64, device=dev)])
+        body = np.asarray(flat, dtype=np.int64) if flat is not None else np.zeros(size, np.int64)
+        return np.concatenate([body, np.array([int(failed)], np.int64)])
 
 
 def torch_allreduce(flat):
@@ -181,7 +208,10 @@ class CountParty(Party):
     def check(self, v, L) -> bool:
         return self._tally(self.tables.consistent(v, L))
 
-    def add_own_and_check(self, P, v, L) -> bool:
+    def precheck(self, inbox):
+        return [None] * len(inbox)  # the count tables are already on the host
+
+    def add_own_and_check(self, P, v, L, pre=None) -> bool:
         L.add(self.own_tuple(P))
         return self.check(v, L)
 

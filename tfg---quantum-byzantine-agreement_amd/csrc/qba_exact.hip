@@ -401,6 +401,47 @@ extern "C" int qba_check_packet_host(qba_ctx *ctx, const uint8_t *li, uint64_t l
   return QBA_OK;
 }
 
+// A round's packets (tfg.py:337-348 -> 289-294) in one host round trip: the
+// k stages concatenated (packet i: [order | rows] of len_i * (m_i + 1)
+// int64, desc[i] = {m_i, len_i, v_i}), ONE H2D through the pinned staging, one
+// qba_check_packet launch per packet, ONE D2H of the concatenated outputs
+// (packet i: len_i + 3 + m_i int64, as qba_check_packet) and one sync.
+extern "C" int qba_check_packets_host(qba_ctx *ctx, const uint8_t *li, uint64_t list_len,
+                                      const int64_t *stage_host, const int64_t *desc, int64_t k, int64_t w,
+                                      int64_t *out_host, qba_stream stream) {
+  if (!ctx || !desc || !out_host || k < 1 || !stage_host)
+    return qba_fail(QBA_EINVAL, "qba_check_packets_host: bad arguments");
+  size_t nin = 0, nout = 0;
+  for (int64_t i = 0; i < k; ++i) {
+    const int64_t m = desc[3 * i], len = desc[3 * i + 1];
+    if (m < 0 || len < 0 || (len && !li))
+      return qba_fail(QBA_EINVAL, "qba_check_packets_host: bad packet descriptor");
+    nin += (size_t)len * (size_t)(m + 1);
+    nout += (size_t)(len + 3 + m);
+  }
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  if ((rc = qba_ensure_staging(ctx, 8 * (nin > nout ? nin : nout), 8 * (nin + nout)))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  int64_t *pin = static_cast<int64_t *>(ctx->pin_h), *d_in = static_cast<int64_t *>(ctx->pin_d),
+          *d_out = d_in + nin;
+  if (nin) {
+    memcpy(pin, stage_host, 8 * nin);
+    QBA_HIP(hipMemcpyAsync(d_in, pin, 8 * nin, hipMemcpyHostToDevice, s));
+  }
+  size_t oi = 0, oo = 0;
+  for (int64_t i = 0; i < k; ++i) {
+    const int64_t m = desc[3 * i], len = desc[3 * i + 1], v = desc[3 * i + 2];
+    if ((rc = qba_check_packet(ctx, li, list_len, d_in + oi, m, len, v, w, d_out + oo, stream))) return rc;
+    oi += (size_t)len * (size_t)(m + 1);
+    oo += (size_t)(len + 3 + m);
+  }
+  QBA_HIP(hipMemcpyAsync(pin, d_out, 8 * nout, hipMemcpyDeviceToHost, s));
+  QBA_HIP(hipStreamSynchronize(s));
+  memcpy(out_host, pin, 8 * nout);
+  return QBA_OK;
+}
+
 // --- wire codec: rawS bits (one int64 per measured bit, MSB first) <-> values ---------
 __global__ void qba_k_bits_to_values(const int64_t *__restrict__ raw, uint64_t count, int nq,
                                      uint8_t *__restrict__ vals) {

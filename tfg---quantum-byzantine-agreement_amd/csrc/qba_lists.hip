@@ -100,6 +100,13 @@ static int dispatch(qba_ctx *ctx, const QbaLaunch &L0) {
     L.count = L0.count - done < ctx->chunk ? L0.count - done : ctx->chunk;
     const uint64_t to_span = PHI_SPAN - ((L0.first + done) & (PHI_SPAN - 1));
     if (L.count > to_span) L.count = to_span;
+    // A chunk that starts off the wide kernels' 8-byte row alignment (the
+    // caller's first column, or the 2^33 split above when first % 8 != 0)
+    // is cut to the next aligned column, so that every later chunk of the
+    // call runs the wide kernel (qba_launch_lists picks the narrow one for
+    // unaligned rows); rows must be aligned to begin with (ld % 8 == 0).
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(L0.lists + done) & 7;
+    if (mis && !(L0.ld & 7) && L.count > 8 - mis) L.count = 8 - mis;
     L.first = L0.first + done;
     L.lists = L0.lists + done;
     L.accumulate = done ? 1 : L0.accumulate;

@@ -776,6 +776,25 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
         }
       }
     }
+#ifdef QBA_EXP_PADVALU  // experiment builds: probe VALU headroom (independent xor chains)
+    {
+      uint32_t z0 = row[0][0], z1 = row[0][1], z2 = row[0][2], z3 = row[0][3];
+      for (int i = 0; i < QBA_EXP_PADVALU / 4; ++i) {
+        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z0) : "v"(row[0][4]));
+        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z1) : "v"(row[0][5]));
+        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z2) : "v"(row[0][6]));
+        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z3) : "v"(row[0][7]));
+      }
+      asm volatile("" ::"v"(z0), "v"(z1), "v"(z2), "v"(z3));
+    }
+#endif
+#ifdef QBA_EXP_PADLDS  // experiment builds: probe LDS headroom (broadcast reads, consumed)
+    {
+      uint32_t z = 0;
+      for (int i = 0; i < QBA_EXP_PADLDS; ++i) z ^= reinterpret_cast<volatile uint32_t *>(hist)[4 * i];
+      asm volatile("" ::"v"(z));
+    }
+#endif
 #ifdef QBA_EXP_NOSTORE
     if (row[0][0] == 0x12345678u && row[0][1] == 0x9abcdef0u)
 #else
@@ -918,6 +937,16 @@ __global__ void QBA_LISTS_BOUNDS
     wq.qn = 0;
     wq.hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     asm("" : "+v"(wq.hoff));  // held in a VGPR (no instruction is emitted)
+#ifdef QBA_EXP_DESYNC  // experiment builds: stagger the waves' phase at the start (s_sleep units of 64 cycles)
+    switch ((threadIdx.x >> 6) % 6) {
+      case 1: __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
+      case 2: __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
+      case 3: for (int i = 0; i < 3; ++i) __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
+      case 4: for (int i = 0; i < 4; ++i) __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
+      case 5: for (int i = 0; i < 5; ++i) __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
+      default: break;
+    }
+#endif
     // wave-uniform trip count: pushes and drains always run with the whole wave
     for (uint32_t u = u0;; u += ustride) {
       const bool act = u < nunits;

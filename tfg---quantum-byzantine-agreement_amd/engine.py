@@ -316,6 +316,40 @@ class Engine:
             ok = True
         return tuple(o[:ln].tolist()), ok
 
+    def check_packets(self, li: torch.Tensor, reqs: Sequence[Tuple[np.ndarray, Sequence, int]],
+                      w: int) -> list:
+        """A round's packets (tfg.py:337-348 -> 289-294) in one device round
+        trip (qba_check_packets_host): reqs = [(order, rows, v)], each as
+        :meth:`check_packet`; returns [(own, ok)] in the same order."""
+        if not reqs:
+            return []
+        dims = [(len(o), len(r)) for o, r, _ in reqs]
+        nin = sum(ln * (m + 1) for ln, m in dims)
+        stage = np.empty(max(nin, 1), np.int64)
+        desc = np.empty(3 * len(reqs), np.int64)
+        off = 0
+        for i, ((order, rows, v), (ln, m)) in enumerate(zip(reqs, dims)):
+            desc[3 * i:3 * i + 3] = (m, ln, int(v))
+            stage[off:off + ln] = order
+            for a, t in enumerate(rows):
+                stage[off + ln * (a + 1):off + ln * (a + 2)] = t if isinstance(t, np.ndarray) else \
+                    np.fromiter(t, dtype=np.int64, count=ln)
+            off += ln * (m + 1)
+        out = np.empty(sum(ln + 3 + m for ln, m in dims), np.int64)
+        call("qba_check_packets_host", self.ctx, _ptr(li), li.numel(), stage.ctypes.data, desc.ctypes.data,
+             len(reqs), int(w), out.ctypes.data, self.stream())
+        res, o = [], 0
+        for ln, m in dims:
+            if out[o + ln]:
+                raise QbaError("qba_check_packets_host: index outside the list")
+            eq = out[o + ln + 3:o + ln + 3 + m]
+            ok = not out[o + ln + 1] and not out[o + ln + 2] and bool(np.all((eq == 0) | (eq == ln)))
+            if m and not ln:  # every tuple empty: the set is {()}, vacuously consistent
+                ok = True
+            res.append((tuple(out[o:o + ln].tolist()), ok))
+            o += ln + 3 + m
+        return res
+
     def check_gather(self, lists: torch.Tensor, count: int, idx: np.ndarray, party: Sequence[int], v: int,
                      w: int) -> bool:
         """consistent(v, L, w) (tfg.py:87-98) over the tuples

@@ -209,6 +209,8 @@ class Comm:
     def Get_size(self) -> int:
         s = C.c_int()
         _check(_init().MPI_Comm_size(self.handle, C.byref(s)), "MPI_Comm_size")
+        if self.handle == COMM_WORLD_HANDLE:
+            check_world_size(s.value)
         return s.value
 
     def Isend(self, buf, dest: int, tag: int = 0) -> Request:
@@ -273,5 +275,19 @@ def load() -> _Module:
 
 
 def launched_by_mpiexec() -> bool:
-    """True when this process is a rank of an mpiexec (Hydra/PMI) launch."""
-    return any(k in os.environ for k in ("PMI_RANK", "PMI_SIZE", "PMI_FD", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_SIZE"))
+    """True when this process is a rank of an MPICH mpiexec (Hydra/PMI)
+    launch.  The binding is MPICH's ABI only (libmpi.so.12, integer handles):
+    an Open MPI launch (OMPI_COMM_WORLD_SIZE) is not recognised here, and
+    :func:`check_world_size` refuses a world whose size disagrees with the
+    launcher's, instead of running N independent single-rank copies."""
+    return any(k in os.environ for k in ("PMI_RANK", "PMI_SIZE", "PMI_FD", "MPI_LOCALRANKID"))
+
+
+def check_world_size(size: int) -> None:
+    """Fail loudly when MPI_Init produced a world that is not the one the
+    launcher started (e.g. a singleton init under a foreign launcher)."""
+    for key in ("PMI_SIZE", "OMPI_COMM_WORLD_SIZE"):
+        want = os.environ.get(key)
+        if want is not None and int(want) != size:
+            raise MPIError(f"MPI_Comm_size is {size} but {key}={want}: this binding speaks MPICH's ABI "
+                           "and was not launched by an MPICH mpiexec")

@@ -110,8 +110,8 @@ class WireCache:
     object: a packet's P and tuples are re-sent to n - 1 ranks and checked
     once, and every conversion of a 31 K-element set or tuple costs ~0.5 ms
     (n = 11, sizeL = 1e6).  Keyed by id(); the entry holds the object, so the
-    id cannot be reused while it is cached; Party.recv clears it, so it holds
-    at most the packet in hand.  Tuples are immutable; the only
+    id cannot be reused while it is cached; the party clears it once per
+    round, so it holds at most one round's packets.  Tuples are immutable; the only
     mutation of a P set is a dishonest rank's ``P.clear()`` (tfg.py:280), which
     the length check catches."""
 
@@ -309,19 +309,43 @@ class Party:
             self.stats.reject += 1
         return ok
 
-    def add_own_and_check(self, P, v, L) -> bool:
+    def _packet_request(self, P, v, L):
+        """(order, rows, v) of one received packet for the device check, and
+        Cond1 (tfg.py:89-92: every received tuple as long as P)."""
+        order = self.wire(P)
+        received = list(L)
+        same_len = all(len(t) == len(order) for t in received)
+        return (order, [self.wire(t) for t in received] if same_len else [], v), same_len
+
+    def precheck(self, inbox):
+        """Device checks of a whole round's inbox in ONE round trip
+        (qba_check_packets_host), before the packets are processed in order:
+        a packet's check depends only on its own P, v and L and this rank's
+        list (a dishonest rank's mutations in lieu_broadcast touch only the
+        objects of the packet being re-sent), so checking them first changes
+        nothing the reference observes.  None when the engine has no batched
+        call (the CPU test engine) or for count mode."""
+        batch = getattr(self.engine, "check_packets", None)
+        if batch is None or not inbox:
+            return [None] * len(inbox)
+        reqs, lens = zip(*(self._packet_request(P, v, L) for P, v, L in inbox))
+        return [(own, ok, same) for (own, ok), same in zip(batch(self.li, list(reqs), self.w), lens)]
+
+    def add_own_and_check(self, P, v, L, pre=None) -> bool:
         """``L.add(tuple(Li[j] for j in P))`` then ``consistent(v, L, w)``
-        (tfg.py:189-192, 291-294): the gather and Cond2/Cond3 run as ONE
-        device launch with one host sync (qba_check_packet); Cond1 and the
-        set bookkeeping stay here."""
+        (tfg.py:189-192, 291-294): the gather and Cond2/Cond3 run on the
+        device (one launch per packet; a round's packets share one host
+        round trip, see precheck); Cond1 and the set bookkeeping stay here."""
+        if pre is not None:
+            own, ok, same_len = pre
+            L.add(own)
+            return self._tally(ok and same_len)
         fast = getattr(self.engine, "check_packet", None)
         if fast is None:  # engines without the fused call (the CPU test engine)
             L.add(self.own_tuple(P))
             return self.check(v, L)
-        order = self.wire(P)
-        received = list(L)
-        same_len = all(len(t) == len(order) for t in received)
-        own, ok = fast(self.li, order, [self.wire(t) for t in received] if same_len else [], v, self.w)
+        (order, rows, _), same_len = self._packet_request(P, v, L)
+        own, ok = fast(self.li, order, rows, v, self.w)
         L.add(own)
         return self._tally(ok and same_len)
 
@@ -330,10 +354,10 @@ class Party:
         send_pvl(self.comm, self.rank, dest, P, v, L, self.dishonest, self.log, self.wire)
 
     def recv(self, src):
-        # a packet is checked and re-sent before the next one is received, so
-        # the cache only ever needs the packet in hand: dropping the previous
-        # one keeps memory at one packet (a 1e7-entry P set is ~20 MB)
-        self.wire.clear()
+        # the wire arrays of the received P / tuples stay cached until the
+        # round is over (Party.run clears the cache at each round start and
+        # comm_broadcast before its receive): a round's inbox is drained
+        # first and its packets are checked and re-sent afterwards
         return recv_pvl(self.comm, self.rank, src, self.wire)
 
     # tfg.py:166-196
@@ -350,6 +374,7 @@ class Party:
                     v = v1 if dest <= int((self.n + 1) / 2) else v2
                 self.send(dest, self.p_for(v), v, set())
         elif self.rank > 1:
+            self.wire.clear()
             P, v, L = self.recv(1)
             ok = self.add_own_and_check(P, v, L)
             self.say(f"[{self.rank}] L = {L}")
@@ -381,8 +406,8 @@ class Party:
                 self.send(dest, P, v, L)
 
     # tfg.py:289-300
-    def lieu_receive(self, P, v, L, rnd):
-        if self.add_own_and_check(P, v, L) and v not in self.Vi and len(L) == rnd + 1:
+    def lieu_receive(self, P, v, L, rnd, pre=None):
+        if self.add_own_and_check(P, v, L, pre) and v not in self.Vi and len(L) == rnd + 1:
             self.Vi.add(v)
             if rnd <= self.n_dis:
                 self.lieu_broadcast(P, v, L)
@@ -401,11 +426,12 @@ class Party:
         status = mpi.Status()
         for rnd in range(1, self.n_dis + 2):
             if self.rank > 1:
+                self.wire.clear()  # the previous round's packets are done with
                 inbox = []
                 while c.Iprobe(source=mpi.ANY_SOURCE, status=status):
                     inbox.append(self.recv(status.Get_source()))
-                for P, v, L in inbox:
-                    self.lieu_receive(P, v, L, rnd)
+                for (P, v, L), pre in zip(inbox, self.precheck(inbox)):
+                    self.lieu_receive(P, v, L, rnd, pre)
             c.Barrier()
         if self.rank > 1 and not self.dishonest:
             self.say(f"[{self.rank}] V{self.rank} = {self.Vi}")
