@@ -212,6 +212,17 @@ QBA_API int qba_check_packets_host(qba_ctx *ctx, const uint8_t *li_dev, uint64_t
                                    const int64_t *stage_host, const int64_t *desc, int64_t k, int64_t w,
                                    int64_t *out_host, qba_stream stream);
 
+/* ---- host-only: the exact-order protocol's set semantics (no device) -------------- */
+/* Iteration order of CPython 3.10's set(keys) for int64 keys inserted in the
+ * given order (tfg.py:240 P = set(buff); tfg.py:182 and 327 set
+ * comprehensions): order_out[*n_out] = the distinct keys in slot order.
+ * Replaces building the Python set and reading it back (tfg.py:189, 209, 291
+ * iterate it).  order_out needs room for n keys. */
+QBA_API int qba_host_pyset_order(const int64_t *keys, int64_t n, int64_t *order_out, int64_t *n_out);
+/* hash(tuple(vals)) of CPython 3.10 (tuplehash over int elements): the set of
+ * tuples L (tfg.py:189, 260, 291) orders and de-duplicates by it. */
+QBA_API int qba_host_pytuple_hash(const int64_t *vals, int64_t n, int64_t *hash_out);
+
 /* ---- wire-compatible codec (rawS layout, tfg.py:81-84, 128-129, 142-161) -------- */
 QBA_API int qba_bits_to_values(qba_ctx *ctx, const int64_t *raw_dev, uint64_t count, int nq,
                        uint8_t *values_dev, qba_stream stream);

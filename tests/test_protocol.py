@@ -93,3 +93,62 @@ def test_wire_cache_and_packet_roundtrip():
     assert wc(t) is buf
     raw = rng.choice(1 << 30, 5000, replace=False).astype(np.int64)
     assert list(set(raw.tolist())) == [int(x) for x in set(raw)]
+
+
+# ---------------------------------------------------------------------------
+# the native restatement of CPython 3.10's set order and tuple hash
+# (qba_host_pyset_order / qba_host_pytuple_hash) against the live interpreter
+# ---------------------------------------------------------------------------
+def test_native_set_order_matches_cpython():
+    import sys
+    protocol = sub("protocol")
+    if sys.version_info[:2] != (3, 10):
+        pytest.skip("the restatement is of CPython 3.10's setobject.c")
+    rng = np.random.default_rng(7)
+    for trial in range(400):
+        n = int(rng.choice([0, 1, 2, 5, 9, 17, 100, 1000, 4999, 31_000, 50_001, 70_000]))
+        hi = int(rng.choice([8, 1000, 10 ** 6, 10 ** 9, 2 ** 62]))
+        keys = rng.integers(0, hi, size=n, dtype=np.int64)
+        if trial % 3 == 0:
+            keys.sort()
+        if trial % 11 == 0:
+            keys = -keys
+        if trial % 7 == 0 and n:
+            keys[::3] = keys[0]  # duplicates collapse
+        want = list(set(keys.tolist()))
+        got = protocol.PSet.build(keys)
+        assert got.arr.tolist() == want, (trial, n, hi)
+        assert repr(got) == repr(set(keys.tolist()))
+    # the reference's own hop: a numpy array straight into set() (numpy scalars)
+    buf = rng.integers(0, 10 ** 6, size=31_000, dtype=np.int64)
+    assert protocol.PSet.build(buf).arr.tolist() == [int(x) for x in set(buf)]
+
+
+def test_native_tuple_hash_and_set_of_tuples_match_cpython():
+    import sys
+    protocol = sub("protocol")
+    if sys.version_info[:2] != (3, 10):
+        pytest.skip("the restatement is of CPython 3.10's tuplehash")
+    rng = np.random.default_rng(8)
+    for _ in range(300):
+        t = rng.integers(-3, 16, size=int(rng.integers(0, 64)), dtype=np.int64)
+        assert hash(protocol.PTuple(t)) == hash(tuple(t.tolist()))
+        assert protocol.PTuple(t) == tuple(t.tolist())
+        assert repr(protocol.PTuple(t)) == repr(tuple(t.tolist()))
+    for _ in range(50):  # L: a set of tuples, with repeats that must collapse
+        rows = [rng.integers(0, 16, size=40, dtype=np.int64) for _ in range(int(rng.integers(1, 8)))]
+        rows += [rows[0].copy()]
+        native = {protocol.PTuple(r) for r in rows}
+        python = {tuple(r.tolist()) for r in rows}
+        assert [tuple(x) for x in native] == list(python)
+        assert repr(native) == repr(python)
+
+
+@pytest.mark.parametrize("name", ["case003", "case013", "case043"])
+def test_protocol_python_sets_path(name, monkeypatch):
+    """The plain-Python set path (any other interpreter, or QBA_PYTHON_SETS=1)
+    gives the same fixture results as the native restatement."""
+    protocol = sub("protocol")
+    monkeypatch.setattr(protocol, "NATIVE_SETS", False)
+    case = next(c for c in CASES if c["name"] == name)
+    _compare(_run(OracleEngine(), case), case["exact"])

@@ -51,6 +51,8 @@ SIGNATURES = {
     "qba_check_packet": [_p, _p, _u64, _p, _i64, _i64, _i64, _i64, _p, _p],
     "qba_check_packet_host": [_p, _p, _u64, _p, _i64, _i64, _i64, _i64, _p, _p],
     "qba_check_packets_host": [_p, _p, _u64, _p, _p, _i64, _i64, _p, _p],
+    "qba_host_pyset_order": [_p, _i64, _p, _p],
+    "qba_host_pytuple_hash": [_p, _i64, _p],
     "qba_lists_to_bits_host": [_p, _p, _u64, C.c_int, _u64, C.c_int, _p, _p],
     "qba_bits_to_values_host": [_p, _p, _u64, C.c_int, _p, _p],
     "qba_rccl_unique_id": [_p],

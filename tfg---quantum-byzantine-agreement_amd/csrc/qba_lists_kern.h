@@ -265,6 +265,9 @@ __device__ __forceinline__ bool qba_accept(uint32_t F, uint32_t T) {
 // (p, h) identify the entry for the rare retry) then qba_closed_finish.
 struct QbaClosed {
   uint32_t nq[4];
+#ifdef QBA_EXP_NQSEL
+  uint32_t nqr[4];  // not-Q words before the nibble mask
+#endif
   uint32_t rank, w0;
 };
 
@@ -280,6 +283,12 @@ __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64
   c.nq[1] = (w1 >> 4) & F::M4;
   c.nq[2] = (w0 >> 4) & F::M4;
   c.nq[3] = 0u;
+#ifdef QBA_EXP_NQSEL
+  c.nqr[0] = c.nq[0];
+  c.nqr[1] = w1 >> 4;
+  c.nqr[2] = w0 >> 4;
+  c.nqr[3] = 0u;
+#endif
   c.w0 = w0;
   const bool o1 = qba_accept<NP>(w1, F::T32);
   uint32_t rank = o1 ? w1 : (w0 & ~31u);
@@ -321,8 +330,19 @@ __device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint
   // for a mask plus a v_cndmask per word
   uint32_t qm = (uint32_t)__builtin_amdgcn_sbfe((int)c.w0, 0, 1);
   asm("" : "+v"(qm));
+#ifdef QBA_EXP_NQSEL  // experiment builds: not-Q words masked by one shared ~qm & M4 (and_or per word)
+  uint32_t nqm = ~qm & F::M4;
+  asm("" : "+v"(nqm));
+#pragma unroll
+  for (int i = 0; i < F::ND; ++i) {
+    uint32_t t = qm & (q[i] ^ R);
+    asm("" : "+v"(t));
+    D[i] = (c.nqr[i] & nqm) | t;
+  }
+#else
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) D[i] = (qm & (q[i] ^ R)) | (~qm & c.nq[i]);
+#endif
 }
 
 // Stage table indices of a rank and the LDS reads.
@@ -508,7 +528,16 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
     if (4 * i + 3 < C::G) mq |= 0xffff0000u;
     U |= (qba_pk_onehot(D[i], one) & mp) | (qba_pk_onehot(D[i] >> 8, one) & mq);
   }
+#ifdef QBA_EXP_DISTFOLD  // experiment builds: lo | hi in one SDWA op (upper half zeroed)
+  {
+    uint32_t r;
+    asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
+        : "=v"(r) : "v"(U));
+    U = r;
+  }
+#else
   U = (U | (U >> 16)) & 0xffffu;
+#endif
   if (__popc(U) != C::G) {  // some pair collides: exact slow path
     // a compact loop (values picked by selects, no private array): this
     // path is rare and unrolling it would multiply the kernel's code size
@@ -794,6 +823,22 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
       for (int i = 0; i < QBA_EXP_PADLDS; ++i) z ^= reinterpret_cast<volatile uint32_t *>(hist)[4 * i];
       asm volatile("" ::"v"(z));
     }
+#endif
+#ifdef QBA_EXP_PACKSTORE  // experiment builds: rows stored as packed nibbles (half the bytes; layout wrong by design)
+    if constexpr (QPT == 2) {
+      if (!TAIL && act) {
+#pragma unroll
+        for (int g = 0; g < C::G; ++g) {
+          uint64_t rb = reinterpret_cast<uint64_t>(lists) + (uint64_t)g * ld;
+          asm("" : "+s"(rb));
+          typedef __attribute__((address_space(1))) uint32_t GU;
+          __builtin_nontemporal_store(row[0][g] | (row[1][g] << 4), reinterpret_cast<GU *>(rb + (c0 >> 1)));
+        }
+      } else if (TAIL) {
+        for (int g = 0; g < C::G; ++g)
+          for (int j = 0; j < valid; ++j) lists[(uint64_t)g * ld + c0 + j] = (uint8_t)(row[0][g] >> (8 * j));
+      }
+    } else
 #endif
 #ifdef QBA_EXP_NOSTORE
     if (row[0][0] == 0x12345678u && row[0][1] == 0x9abcdef0u)
@@ -1157,7 +1202,7 @@ __global__ void __launch_bounds__(256)
 #ifndef QBA_GRID_QPT
 #define QBA_GRID_QPT 2
 #endif
-static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count) {
+static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count, int qpt = QBA_GRID_QPT) {
   // the occupancy query costs tens of microseconds: cached per (kernel, LDS)
   struct Occ {
     const void *k;
@@ -1179,7 +1224,7 @@ static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count) 
   const uint64_t nquad = (count + 3) >> 2;
   // >= 2 quads (one wide thread-step) per thread: a small launch (configs[1],
   // 1e6 entries) spreads over 163 workgroups instead of 82
-  uint64_t g = (nquad + QBA_GRID_QPT * QBA_LBLOCK - 1) / (QBA_GRID_QPT * QBA_LBLOCK);
+  uint64_t g = (nquad + qpt * QBA_LBLOCK - 1) / (qpt * QBA_LBLOCK);
   const uint64_t cap = (uint64_t)ctx->num_cus * (uint64_t)per_cu;
 #ifdef QBA_EXP_GRID  // experiment builds: grid from the environment (QBA_EXP_GRID=<workgroups>)
   if (const char *e = getenv("QBA_EXP_GRID")) g = strtoull(e, nullptr, 10);
@@ -1234,7 +1279,12 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   const bool wide = false;
 #else
   constexpr uintptr_t VA = 4 * QBA_WIDE_QPT - 1;  // row vectors need their natural alignment
-  const bool wide = !(reinterpret_cast<uintptr_t>(L.lists) & VA) && !(L.ld & VA);
+#ifdef QBA_EXP_SMALLNARROW  // experiment builds: launches below this many entries take the narrow kernel on a wider grid
+  const bool small = L.count < (uint64_t)QBA_EXP_SMALLNARROW;
+#else
+  const bool small = false;
+#endif
+  const bool wide = !small && !(reinterpret_cast<uintptr_t>(L.lists) & VA) && !(L.ld & VA);
 #endif
 #define QBA_K(M, S) (wide ? (const void *)qba_k_lists<NP, M, S, QBA_WIDE_QPT> : (const void *)qba_k_lists<NP, M, S, 1>)
   const void *kern = nullptr;
@@ -1252,7 +1302,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   }
 #undef QBA_K
   if (lds > 65536) QBA_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const int grid = grid_for(ctx, kern, lds, L.count);
+  const int grid = grid_for(ctx, kern, lds, L.count, wide ? QBA_GRID_QPT : 1);
   uint32_t *slab = nullptr;
   if (L.mode != 0) {
     int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBP * sizeof(uint32_t));

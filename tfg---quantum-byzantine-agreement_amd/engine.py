@@ -320,7 +320,8 @@ class Engine:
                       w: int) -> list:
         """A round's packets (tfg.py:337-348 -> 289-294) in one device round
         trip (qba_check_packets_host): reqs = [(order, rows, v)], each as
-        :meth:`check_packet`; returns [(own, ok)] in the same order."""
+        :meth:`check_packet`; returns [(own, ok, own_wire)] in the same order
+        (own_wire: the own tuple as the int64 array it travels as)."""
         if not reqs:
             return []
         dims = [(len(o), len(r)) for o, r, _ in reqs]
@@ -346,7 +347,8 @@ class Engine:
             ok = not out[o + ln + 1] and not out[o + ln + 2] and bool(np.all((eq == 0) | (eq == ln)))
             if m and not ln:  # every tuple empty: the set is {()}, vacuously consistent
                 ok = True
-            res.append((tuple(out[o:o + ln].tolist()), ok))
+            own = out[o:o + ln]
+            res.append((tuple(own.tolist()), ok, own))
             o += ln + 3 + m
         return res
 

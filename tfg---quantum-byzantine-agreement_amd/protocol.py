@@ -28,6 +28,9 @@ Rounds use the host's comm: real mpi4py under ``mpiexec``, or
 """
 from __future__ import annotations
 
+import ctypes as C
+import os
+import sys
 import threading
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
@@ -35,6 +38,7 @@ from typing import Callable, Dict, List, Optional
 import numpy as np
 
 from . import comm as comm_mod
+from ._lib import call
 from .resource import n_qubits
 
 
@@ -88,7 +92,7 @@ def consistent(v, L, w, engine=None):
         return False
     if engine is None:
         raise RuntimeError("consistent needs an Engine (no CPU fallback)")
-    rows = np.array([list(t) for t in L], dtype=np.int64).reshape(len(L), length)
+    rows = np.array([t.arr if isinstance(t, PTuple) else list(t) for t in L], dtype=np.int64).reshape(len(L), length)
     return engine.consistent_rows(rows, int(v), int(w))
 
 
@@ -102,7 +106,97 @@ def decide_order(Vi, v, is_comm):
 # ---------------------------------------------------------------------------
 def _wire(x) -> np.ndarray:
     """int64 array of a set / tuple in its iteration order (the wire order)."""
+    arr = getattr(x, "arr", None)
+    if arr is not None:  # PSet / PTuple: the order is kept as the array itself
+        return arr
     return np.fromiter(x, dtype=np.int64, count=len(x))
+
+
+# ---------------------------------------------------------------------------
+# P sets and L tuples as CPython 3.10 holds them, without the Python objects
+# (qba_host_pyset_order / qba_host_pytuple_hash restate setobject.c and
+# tuplehash; tests/test_protocol.py compares them with the live interpreter).
+# A 31 K-element P (n = 11, sizeL = 1e6) then costs one native pass instead of
+# a Python set build plus its conversion back to an array at every hop.
+# ---------------------------------------------------------------------------
+NATIVE_SETS = sys.version_info[:2] == (3, 10) and os.environ.get("QBA_PYTHON_SETS") != "1"
+
+
+class PSet:
+    """A packet's P: the int64 array of set(insertion sequence) in CPython's
+    iteration order (tfg.py:182, 240, 327).  Supports what tfg.py does with
+    P: len, iteration, clear (tfg.py:280) and its repr in the logs."""
+
+    __slots__ = ("arr",)
+
+    def __init__(self, order: np.ndarray):
+        self.arr = order
+
+    @classmethod
+    def build(cls, seq) -> "PSet":
+        seq = np.ascontiguousarray(seq, dtype=np.int64)
+        out = np.empty(max(len(seq), 1), np.int64)
+        got = C.c_int64()
+        call("qba_host_pyset_order", seq.ctypes.data, len(seq), out.ctypes.data, C.byref(got))
+        return cls(out[:got.value])
+
+    def __len__(self) -> int:
+        return len(self.arr)
+
+    def __iter__(self):
+        return iter(self.arr.tolist())
+
+    def clear(self) -> None:
+        self.arr = self.arr[:0]
+
+    def __repr__(self) -> str:
+        return "{" + ", ".join(map(str, self.arr.tolist())) + "}" if len(self.arr) else "set()"
+
+
+class PTuple:
+    """An L tuple held as its int64 array; hashes and compares as the Python
+    tuple of the same ints, so a set of them orders and de-duplicates as
+    tfg.py's set of tuples does (tfg.py:189, 260, 291)."""
+
+    __slots__ = ("arr", "_h")
+
+    def __init__(self, arr: np.ndarray):
+        self.arr = arr
+        h = C.c_int64()
+        call("qba_host_pytuple_hash", arr.ctypes.data, len(arr), C.byref(h))
+        self._h = h.value
+
+    def __hash__(self) -> int:
+        return self._h
+
+    def __eq__(self, other) -> bool:
+        if isinstance(other, PTuple):
+            return self._h == other._h and len(self.arr) == len(other.arr) and bool(np.array_equal(self.arr, other.arr))
+        if isinstance(other, tuple):
+            return tuple(self.arr.tolist()) == other
+        return NotImplemented
+
+    def __len__(self) -> int:
+        return len(self.arr)
+
+    def __iter__(self):
+        return iter(self.arr.tolist())
+
+    def __repr__(self) -> str:
+        return repr(tuple(self.arr.tolist()))
+
+
+def make_pset(seq):
+    """set(seq) as tfg.py builds it (PSet when the native restatement applies)."""
+    if NATIVE_SETS:
+        return PSet.build(seq)
+    return set(np.asarray(seq, dtype=np.int64).tolist())
+
+
+def make_tuple(arr: np.ndarray):
+    """tuple(arr) as tfg.py builds it (PTuple when the native restatement applies)."""
+    arr = np.ascontiguousarray(arr, dtype=np.int64)
+    return PTuple(arr) if NATIVE_SETS else tuple(arr.tolist())
 
 
 class WireCache:
@@ -167,15 +261,15 @@ def recv_pvl(comm, rank, src, wire: Optional["WireCache"] = None):
     own order, so the received buffer becomes its cached wire array (P's
     iteration order differs from the wire order: the set hop, tfg.py:209)."""
     n_p = int(_recv_array(comm, src, 1, 1)[0])
-    P = set(_recv_array(comm, src, 2, n_p).tolist())
+    P = make_pset(_recv_array(comm, src, 2, n_p))
     v = _recv_array(comm, src, 3, 1)[0]
     n_l = int(_recv_array(comm, src, 4, 1)[0])
     L = set()
     for i in range(n_l):
         ln = int(_recv_array(comm, src, 5 + 2 * i, 1)[0])
         buf = _recv_array(comm, src, 6 + 2 * i, ln)
-        t = tuple(buf.tolist())
-        if wire is not None:
+        t = make_tuple(buf)
+        if wire is not None and not NATIVE_SETS:
             wire.put(t, buf)
         L.add(t)
     return P, v, L
@@ -280,7 +374,7 @@ class Party:
 
     # tfg.py:327-330
     def commander_setup(self):
-        self.isq = set(self.engine.isq_indices(self.li, self.lc).tolist())
+        self.isq = make_pset(self.engine.isq_indices(self.li, self.lc))
         self.say("isQCorr = ", self.isq)
         self.v = self.rng.randint(self.w)
         self.say("v =", self.v)
@@ -289,14 +383,12 @@ class Party:
         """{x for x in isQCorr if Lc[x] == v} in isQCorr's iteration order (tfg.py:182)."""
         key = int(v)
         if key not in self._p_cache:
-            order = np.fromiter(self.isq, dtype=np.int64, count=len(self.isq))
-            self._p_cache[key] = self.engine.select_eq(order, self.lc, key).tolist()
-        return set(self._p_cache[key])
+            self._p_cache[key] = np.asarray(self.engine.select_eq(_wire(self.isq), self.lc, key), dtype=np.int64)
+        return make_pset(self._p_cache[key])
 
     def own_tuple(self, P) -> tuple:
         """tuple(Li[j] for j in P) in this process's iteration order of P (tfg.py:189, 291)."""
-        order = np.fromiter(P, dtype=np.int64, count=len(P))
-        return tuple(self.engine.gather(self.li, order).tolist())
+        return make_tuple(self.engine.gather(self.li, _wire(P)))
 
     def check(self, v, L) -> bool:
         ok = consistent(v, L, self.w, self.engine)
@@ -329,7 +421,8 @@ class Party:
         if batch is None or not inbox:
             return [None] * len(inbox)
         reqs, lens = zip(*(self._packet_request(P, v, L) for P, v, L in inbox))
-        return [(own, ok, same) for (own, ok), same in zip(batch(self.li, list(reqs), self.w), lens)]
+        return [(make_tuple(arr) if NATIVE_SETS else own, ok, same, arr)
+                for (own, ok, arr), same in zip(batch(self.li, list(reqs), self.w), lens)]
 
     def add_own_and_check(self, P, v, L, pre=None) -> bool:
         """``L.add(tuple(Li[j] for j in P))`` then ``consistent(v, L, w)``
@@ -337,7 +430,9 @@ class Party:
         device (one launch per packet; a round's packets share one host
         round trip, see precheck); Cond1 and the set bookkeeping stay here."""
         if pre is not None:
-            own, ok, same_len = pre
+            own, ok, same_len, arr = pre
+            if not NATIVE_SETS:
+                self.wire.put(own, arr)  # its wire array, if it is re-sent (no re-conversion)
             L.add(own)
             return self._tally(ok and same_len)
         fast = getattr(self.engine, "check_packet", None)
@@ -346,6 +441,8 @@ class Party:
             return self.check(v, L)
         (order, rows, _), same_len = self._packet_request(P, v, L)
         own, ok = fast(self.li, order, rows, v, self.w)
+        if NATIVE_SETS:
+            own = make_tuple(np.array(own, dtype=np.int64))
         L.add(own)
         return self._tally(ok and same_len)
 
