@@ -161,11 +161,43 @@ static void check_perm_tables() {
   CHECK(qba_perm_tables(12, nullptr, 0, sizes) == QBA_EINVAL, "n=12 accepted");
 }
 
+// qba_host.cpp (CPython set order / tuple hash restatement) on random key
+// sequences: the order is a permutation of the distinct keys, nothing is
+// read or written outside the buffers (ASan), no signed overflow (UBSan);
+// bad arguments are refused.  Equality with the live interpreter is checked
+// by tests/test_protocol.py.
+extern "C" int qba_host_pyset_order(const int64_t *keys, int64_t n, int64_t *order_out, int64_t *n_out);
+extern "C" int qba_host_pytuple_hash(const int64_t *vals, int64_t n, int64_t *hash_out);
+static void check_host_sets(std::mt19937_64 &rng) {
+  for (int trial = 0; trial < 200; ++trial) {
+    const int64_t n = (int64_t)(rng() % 80000);
+    std::vector<int64_t> keys(n);
+    const int64_t span = trial % 4 == 0 ? 16 : trial % 4 == 1 ? 1000000 : trial % 4 == 2 ? (1ll << 62) : 64;
+    for (auto &k : keys) k = (int64_t)(rng() % (uint64_t)span) * (trial % 5 == 0 ? -1 : 1);
+    if (trial == 7 && n) keys[0] = INT64_MIN;
+    std::vector<int64_t> out(n + 1);
+    int64_t m = -1;
+    CHECK(qba_host_pyset_order(keys.data(), n, out.data(), &m) == 0, "pyset_order rc");
+    std::vector<int64_t> a(keys), b(out.begin(), out.begin() + (m < 0 ? 0 : m));
+    std::sort(a.begin(), a.end());
+    a.erase(std::unique(a.begin(), a.end()), a.end());
+    std::sort(b.begin(), b.end());
+    CHECK(a == b, "pyset_order is not a permutation of the distinct keys (trial %d)", trial);
+    int64_t h = 0;
+    CHECK(qba_host_pytuple_hash(keys.data(), n, &h) == 0, "pytuple_hash rc");
+  }
+  int64_t m = 0, h = 0;
+  CHECK(qba_host_pyset_order(nullptr, 3, nullptr, &m) != 0, "pyset_order accepted NULL keys");
+  CHECK(qba_host_pyset_order(nullptr, 0, nullptr, &m) == 0 && m == 0, "empty set");
+  CHECK(qba_host_pytuple_hash(nullptr, -1, &h) != 0, "pytuple_hash accepted n < 0");
+}
+
 int main() {
   std::mt19937_64 rng(20261016);
   check_alias(rng);
   check_circuits(rng);
   check_perm_tables();
+  check_host_sets(rng);
   if (failures) {
     fprintf(stderr, "%d check(s) failed\n", failures);
     return 1;
