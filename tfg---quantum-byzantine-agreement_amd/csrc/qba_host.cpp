@@ -72,11 +72,84 @@ void insert_clean(std::vector<Slot> &t, size_t mask, int64_t key, int64_t hash) 
   }
 }
 
+// The protocol's keys are list positions: 0 <= key < 2^61 - 1, where
+// hash(key) == key.  The table then holds the keys alone (8 B per slot,
+// -1 = empty): the same probe sequence as the general form below.
+void insert_clean_nat(std::vector<int64_t> &t, size_t mask, int64_t key) {
+  size_t perturb = (size_t)key;
+  size_t i = (size_t)key & mask;
+  for (;;) {
+    if (t[i] < 0) {
+      t[i] = key;
+      return;
+    }
+    if (i + kLinearProbes <= mask) {
+      for (size_t j = 1; j <= kLinearProbes; ++j)
+        if (t[i + j] < 0) {
+          t[i + j] = key;
+          return;
+        }
+    }
+    perturb >>= kPerturbShift;
+    i = (i * 5 + 1 + perturb) & mask;
+  }
+}
+
+int64_t pyset_order_nat(const int64_t *keys, int64_t n, int64_t *order_out) {
+  size_t mask = kMinSize - 1, fill = 0;
+  std::vector<int64_t> t(kMinSize, -1);
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t key = keys[k];
+    size_t perturb = (size_t)key;
+    size_t i = (size_t)key & mask;
+    bool present = false, placed = false;
+    while (!placed && !present) {
+      size_t probes = (i + kLinearProbes <= mask) ? kLinearProbes : 0;
+      for (size_t j = i;; ++j) {
+        const int64_t e = t[j];
+        if (e < 0) {
+          t[j] = key;
+          ++fill;
+          placed = true;
+          break;
+        }
+        if (e == key) {
+          present = true;
+          break;
+        }
+        if (probes-- == 0) break;
+      }
+      if (placed || present) break;
+      perturb >>= kPerturbShift;
+      i = (i * 5 + 1 + perturb) & mask;
+    }
+    if (present || fill * 5 < mask * 3) continue;  // no deletions: fill == used
+    const size_t minused = fill > 50000 ? fill * 2 : fill * 4;
+    size_t newsize = kMinSize;
+    while (newsize <= minused) newsize <<= 1;
+    std::vector<int64_t> nt(newsize, -1);
+    for (const int64_t e : t)
+      if (e >= 0) insert_clean_nat(nt, newsize - 1, e);
+    t.swap(nt);
+    mask = newsize - 1;
+  }
+  int64_t m = 0;
+  for (const int64_t e : t)
+    if (e >= 0) order_out[m++] = e;
+  return m;
+}
+
 }  // namespace
 
 extern "C" int qba_host_pyset_order(const int64_t *keys, int64_t n, int64_t *order_out, int64_t *n_out) {
   if (n < 0 || !n_out || (n > 0 && (!keys || !order_out)))
     return qba_fail(QBA_EINVAL, "qba_host_pyset_order: bad arguments");
+  bool natural = true;
+  for (int64_t k = 0; k < n && natural; ++k) natural = keys[k] >= 0 && (uint64_t)keys[k] < kM61;
+  if (natural) {
+    *n_out = pyset_order_nat(keys, n, order_out);
+    return QBA_OK;
+  }
   size_t mask = kMinSize - 1, fill = 0, used = 0;
   std::vector<Slot> t(kMinSize, Slot{0, 0, false});
   for (int64_t k = 0; k < n; ++k) {
