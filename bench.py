@@ -343,16 +343,14 @@ def config0(args, eng):
                   "traffic": None, "note": "host protocol rounds; per-packet device calls"}, extra)
 
 
-def _config1_graph(args, eng, n, count, lists, counts, overlap):
-    """K sample_check passes of configs[1] captured in one hipGraph and
-    replayed; (wall s, device s) per pass.  overlap: each pass's slab
-    reduction runs on the engine's own stream while the next pass samples
-    (qba_async_reduce; two slabs alternate, joined before the graph ends)."""
+def config1(args, eng):
+    """configs[1]: n=11, sizeL=1e6 on one GPU; K steps in one hipGraph."""
     import torch
-    eng.async_reduce(overlap)
-    for _ in range(2):  # allocates the scratch (both slabs) before the capture
-        eng.sample_check(n, args.seed, 0, count, lists, counts)
-    eng.join_reduce()
+    n, count = 11, 1_000_000
+    info = eng.prepare(n)
+    lists = eng.alloc_lists(n, count)
+    counts = eng.alloc_counts(n)
+    eng.sample_check(n, args.seed, 0, count, lists, counts)  # allocates scratch before capture
     torch.cuda.synchronize()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -361,7 +359,6 @@ def _config1_graph(args, eng, n, count, lists, counts, overlap):
         with torch.cuda.graph(g, stream=s):
             for _ in range(args.steps):
                 eng.sample_check(n, args.seed, 0, count, lists, counts)
-            eng.join_reduce()
     torch.cuda.synchronize()
     for _ in range(max(1, args.warmup)):
         g.replay()
@@ -374,32 +371,13 @@ def _config1_graph(args, eng, n, count, lists, counts, overlap):
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / args.steps
     dev = a.elapsed_time(b) * 1e-3 / args.steps
-    eng.async_reduce(False)
-    return wall, dev
-
-
-def config1(args, eng):
-    """configs[1]: n=11, sizeL=1e6 on one GPU; K passes in one hipGraph, each
-    pass's slab reduction overlapped with the next pass (the serial chain --
-    list kernel then reduction -- is reported beside it)."""
-    import torch
-    n, count = 11, 1_000_000
-    info = eng.prepare(n)
-    lists = eng.alloc_lists(n, count)
-    counts = eng.alloc_counts(n)
-    serial_wall, serial_dev = _config1_graph(args, eng, n, count, lists, counts, overlap=False)
-    ref = [x.clone() for x in (counts.H, counts.C, counts.P)]
-    wall, dev = _config1_graph(args, eng, n, count, lists, counts, overlap=True)
-    torch.cuda.synchronize()
-    same = all(torch.equal(x, y) for x, y in zip(ref, (counts.H, counts.C, counts.P)))
     ach = 24 * count / dev / 1e9
-    extra = {"ms_per_step": wall * 1e3, "serial_ms_per_step": serial_wall * 1e3,
-             "overlap_counts_equal_serial": bool(same)}
+    extra = {"ms_per_step": wall * 1e3}
     if not args.no_cpu_baseline:
         extra["cpu_baseline"] = cpu_baseline_counts(n, args.seed, info, args.cpu_seconds / 2)
     return _line(args, count / wall, "entries/s",
                  "BASELINE configs[1]: n=11 parties, 3 dishonest, sizeL=1e6 on one GPU "
-                 f"({args.steps} passes in one hipGraph, reduction overlapped with the next pass)",
+                 f"({args.steps} steps in one hipGraph)",
                  {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": ach / HBM_PEAK_GBS, "traffic": None,
                   "note": "12 MB of lists stay in the 256 MB Infinity Cache; launch-bound"}, extra)

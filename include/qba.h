@@ -73,18 +73,6 @@ QBA_API int qba_destroy(qba_ctx *ctx);
 /* Pre-allocate scratch for counts launches of up to `max_blocks` workgroups so
  * that later calls never allocate (required before hipGraph capture). */
 QBA_API int qba_reserve(qba_ctx *ctx, int n_parties, int64_t max_blocks);
-/* Overlapped reduction (configs[1]-sized, launch-latency-bound passes): with
- * enable = 1, a counting launch's slab reduction (qba_k_reduce) and the
- * zeroing of its H/C/P run on the context's own stream, ordered after the
- * launch's list kernel, while the caller's stream goes on to its next launch
- * (two slabs alternate; a list kernel waits only for the reduction that last
- * read its slab).  H/C/P of a call are complete once qba_join_reduce has
- * made the reading stream wait for the context's stream (also required
- * before the end of a hipGraph capture that recorded such launches).  After
- * a join, the next counting launch goes on the joined stream, or follows a
- * synchronisation (e.g. before a capture begins on another stream). */
-QBA_API int qba_async_reduce(qba_ctx *ctx, int enable);
-QBA_API int qba_join_reduce(qba_ctx *ctx, qba_stream stream);
 
 /* ---- (A1/A2) resource preparation: dense fp64 statevector, gfx950 kernels --------- */
 /* Replaces qs.QGate(...).add_operation(...) + qs.Drewom().execute(...) state

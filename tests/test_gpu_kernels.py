@@ -708,58 +708,3 @@ def test_invalid_arguments_leave_context_usable(engine):
     assert np.array_equal(got[:, :count].cpu().numpy(), ref)
     H, C, P, _ = oracle_lib.counts(ref, n)
     assert np.array_equal(c.numpy()[0], H)
-
-
-def test_async_reduce_equals_serial(engine):
-    """qba_async_reduce: each counting call's reduction runs on the context's
-    own stream (two alternating slabs); consecutive calls into different and
-    into the SAME count buffers, a call split into several launches
-    (accumulate), and a hipGraph capture give exactly the serial results."""
-    n, count = 11, 1_000_003
-    info = engine.prepare(n)
-    lists = engine.alloc_lists(n, count)
-    seeds = [3, 4, 5, 6, 7]
-    serial = []
-    for sd in seeds:
-        _, c = engine.sample_check(n, sd, 17, count, lists)
-        serial.append([x.clone() for x in (c.H, c.C, c.P)])
-    torch.cuda.synchronize()
-    H, C, P, bad = oracle_lib.stream_counts(n, seeds[-1], 17, count, info["notq"], info["q"], info["closed"])
-    assert bad == 0 and np.array_equal(serial[-1][0].cpu().numpy(), H) and np.array_equal(serial[-1][2].cpu().numpy(), P)
-    engine.async_reduce(True)
-    try:
-        outs = [engine.alloc_counts(n) for _ in seeds]
-        for sd, c in zip(seeds, outs):  # distinct buffers
-            engine.sample_check(n, sd, 17, count, lists, c)
-        same = engine.alloc_counts(n)
-        for sd in seeds:  # one buffer, rewritten by every call: ends as the last seed's counts
-            engine.sample_check(n, sd, 17, count, lists, same)
-        engine.join_reduce()
-        torch.cuda.synchronize()
-        for c, want in zip(outs, serial):
-            assert all(torch.equal(x, y) for x, y in zip((c.H, c.C, c.P), want))
-        assert all(torch.equal(x, y) for x, y in zip((same.H, same.C, same.P), serial[-1]))
-        # several launches per call (chunks of 300 001 entries: accumulate into the outputs)
-        flat = engine.count_tables(n, count, seeds[0], chunk=300_001, first=17)
-        ref = np.concatenate([t.cpu().numpy().ravel() for t in serial[0]])
-        assert np.array_equal(flat, ref)
-        # captured in a graph, joined before the capture ends
-        g_counts = engine.alloc_counts(n)
-        engine.sample_check(n, seeds[1], 17, count, lists, g_counts)
-        engine.join_reduce()
-        torch.cuda.synchronize()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                for sd in seeds[1:3]:
-                    engine.sample_check(n, sd, 17, count, lists, g_counts)
-                engine.join_reduce()
-        g.replay()
-        torch.cuda.synchronize()
-        assert all(torch.equal(x, y) for x, y in zip((g_counts.H, g_counts.C, g_counts.P), serial[2]))
-    finally:
-        engine.join_reduce()
-        torch.cuda.synchronize()
-        engine.async_reduce(False)

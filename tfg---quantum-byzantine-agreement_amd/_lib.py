@@ -32,8 +32,6 @@ SIGNATURES = {
     "qba_init": [C.c_int, C.POINTER(_p)],
     "qba_destroy": [_p],
     "qba_reserve": [_p, C.c_int, _i64],
-    "qba_async_reduce": [_p, C.c_int],
-    "qba_join_reduce": [_p, _p],
     "qba_sv_init": [_p, _p, C.c_int, _p],
     "qba_sv_apply": [_p, _p, C.c_int, _pi32, C.c_int, _p],
     "qba_sv_prepare": [_p, _p, C.c_int, _pi32, C.c_int, _p],

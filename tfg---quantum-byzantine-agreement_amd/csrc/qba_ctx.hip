@@ -64,16 +64,6 @@ extern "C" int qba_destroy(qba_ctx *ctx) {
     if (ctx->prog_dev[n]) (void)hipFree(ctx->prog_dev[n]);
     free(ctx->prog_host[n]);
   }
-  if (ctx->red_stream) {
-    (void)hipStreamSynchronize(ctx->red_stream);
-    (void)hipStreamDestroy(ctx->red_stream);
-    for (int s = 0; s < 2; ++s) {
-      (void)hipEventDestroy(ctx->list_done[s]);
-      (void)hipEventDestroy(ctx->red_done[s]);
-    }
-  }
-  for (int s = 0; s < 2; ++s)
-    if (ctx->aslab[s]) (void)hipFree(ctx->aslab[s]);
   if (ctx->slab) (void)hipFree(ctx->slab);
   if (ctx->scan) (void)hipFree(ctx->scan);
   if (ctx->flag) (void)hipFree(ctx->flag);
@@ -101,52 +91,6 @@ static int ensure(void *&ptr, size_t &have, size_t want, const char *what) {
 }
 
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes) { return ensure(ctx->slab, ctx->slab_bytes, bytes, "slab"); }
-int qba_async_slab(qba_ctx *ctx, int s, size_t bytes) {
-  return ensure(ctx->aslab[s], ctx->aslab_bytes[s], bytes, "slab");
-}
-
-// Overlapped slab reduction (see qba.h).  Enabling creates the context's
-// reduce stream and its events; disabling first waits for it.
-extern "C" int qba_async_reduce(qba_ctx *ctx, int enable) {
-  if (!ctx) return qba_fail(QBA_EINVAL, "qba_async_reduce: ctx is NULL");
-  int rc = qba_set_device(ctx);
-  if (rc) return rc;
-  if (enable && !ctx->red_stream) {
-    QBA_HIP(hipStreamCreateWithFlags(&ctx->red_stream, hipStreamNonBlocking));
-    for (int s = 0; s < 2; ++s) {
-      QBA_HIP(hipEventCreateWithFlags(&ctx->list_done[s], hipEventDisableTiming));
-      QBA_HIP(hipEventCreateWithFlags(&ctx->red_done[s], hipEventDisableTiming));
-      ctx->red_recorded[s] = false;
-    }
-    ctx->next_slab = 0;
-  } else if (!enable && ctx->red_stream) {
-    QBA_HIP(hipStreamSynchronize(ctx->red_stream));
-    QBA_HIP(hipStreamDestroy(ctx->red_stream));
-    for (int s = 0; s < 2; ++s) {
-      QBA_HIP(hipEventDestroy(ctx->list_done[s]));
-      QBA_HIP(hipEventDestroy(ctx->red_done[s]));
-    }
-    ctx->red_stream = nullptr;
-  }
-  return QBA_OK;
-}
-
-extern "C" int qba_join_reduce(qba_ctx *ctx, qba_stream stream) {
-  if (!ctx) return qba_fail(QBA_EINVAL, "qba_join_reduce: ctx is NULL");
-  if (!ctx->red_stream) return QBA_OK;
-  int rc = qba_set_device(ctx);
-  if (rc) return rc;
-  // The joined stream now carries both reductions: later launches on it are
-  // ordered after them, so the slab guards are dropped (a hipGraph capture
-  // begun on it after a synchronisation then never waits on an event
-  // recorded outside the capture).
-  for (int s = 0; s < 2; ++s)
-    if (ctx->red_recorded[s]) {
-      QBA_HIP(hipStreamWaitEvent((hipStream_t)stream, ctx->red_done[s], 0));
-      ctx->red_recorded[s] = false;
-    }
-  return QBA_OK;
-}
 int qba_ensure_scan(qba_ctx *ctx, size_t bytes) { return ensure(ctx->scan, ctx->scan_bytes, bytes, "scan"); }
 
 // pinned host staging (hipHostMalloc) + device staging for the synchronous

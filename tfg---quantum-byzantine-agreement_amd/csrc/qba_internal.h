@@ -188,18 +188,7 @@ struct qba_ctx {
   // RCCL communicator of the GPU-owner ranks (qba_rccl_init), or null
   void *rccl_comm = nullptr;
   int rccl_ranks = 0;
-  // overlapped reduction (qba_async_reduce): a counting launch's slab
-  // reduction runs on this context's own stream while the caller's stream
-  // goes on to the next launch; two slabs alternate, each guarded by the
-  // event of the reduction that last read it
-  hipStream_t red_stream = nullptr;
-  hipEvent_t list_done[2] = {}, red_done[2] = {};
-  bool red_recorded[2] = {};
-  void *aslab[2] = {};
-  size_t aslab_bytes[2] = {};
-  int next_slab = 0;
 };
-int qba_async_slab(qba_ctx *ctx, int s, size_t bytes);
 void qba_rccl_release(qba_ctx *ctx);
 
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes);

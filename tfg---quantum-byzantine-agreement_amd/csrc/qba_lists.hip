@@ -165,10 +165,7 @@ extern "C" int qba_reserve(qba_ctx *ctx, int n, int64_t max_blocks) {
     return qba_fail(QBA_EINVAL, "qba_reserve: bad arguments");
   int rc = qba_set_device(ctx);
   if (rc) return rc;
-  const size_t bytes = (size_t)max_blocks * nbins_of(n) * sizeof(uint32_t);
-  if (ctx->red_stream)  // overlapped reduction: both alternating slabs
-    for (int s = 0; s < 2 && !rc; ++s) rc = qba_async_slab(ctx, s, bytes);
-  return rc ? rc : qba_ensure_slab(ctx, bytes);
+  return qba_ensure_slab(ctx, (size_t)max_blocks * nbins_of(n) * sizeof(uint32_t));
 }
 
 // ---------------------------------------------------------------------------

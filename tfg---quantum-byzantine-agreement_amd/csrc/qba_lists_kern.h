@@ -1304,16 +1304,10 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   if (lds > 65536) QBA_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int grid = grid_for(ctx, kern, lds, L.count, wide ? QBA_GRID_QPT : 1);
   uint32_t *slab = nullptr;
-  // overlapped reduction (qba_async_reduce): alternate slabs, the reduction on
-  // the context's stream; the outputs are zeroed there too, in order with it
-  const bool async = L.mode != 0 && ctx->red_stream != nullptr;
-  const int sl = ctx->next_slab;
   if (L.mode != 0) {
-    const size_t bytes = (size_t)grid * C::NBP * sizeof(uint32_t);
-    int rc = async ? qba_async_slab(ctx, sl, bytes) : qba_ensure_slab(ctx, bytes);
+    int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBP * sizeof(uint32_t));
     if (rc) return rc;
-    slab = reinterpret_cast<uint32_t *>(async ? ctx->aslab[sl] : ctx->slab);
-    if (async && ctx->red_recorded[sl]) QBA_HIP(hipStreamWaitEvent(L.stream, ctx->red_done[sl], 0));
+    slab = reinterpret_cast<uint32_t *>(ctx->slab);
   }
   const uint32_t k0 = (uint32_t)L.seed, k1 = (uint32_t)(L.seed >> 32);
   const QbaProgramSet *ps = L.ps;
@@ -1321,33 +1315,15 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   uint32_t count = (uint32_t)L.count;
   uint8_t *lists = L.lists;
   uint64_t ld = L.ld;
-  const uint32_t zflags =
-      (L.mode != 0 && !L.accumulate ? 1u : 0u) | (L.mode != 0 && !L.stats_accumulate ? 2u : 0u);
-  QbaZero zero{L.H, L.C, L.P, L.stats, async ? 0u : zflags};
+  QbaZero zero{L.H, L.C, L.P, L.stats,
+               (L.mode != 0 && !L.accumulate ? 1u : 0u) | (L.mode != 0 && !L.stats_accumulate ? 2u : 0u)};
   void *args[] = {&ps, (void *)&k0, (void *)&k1, &first, &count, &lists, &ld, &slab, &zero};
   QBA_HIP(hipLaunchKernel(kern, dim3(grid), dim3(QBA_LBLOCK), args, lds, L.stream));
   QBA_HIP(hipGetLastError());
   if (L.mode == 0) return QBA_OK;
-  hipStream_t rs = L.stream;
-  if (async) {
-    rs = ctx->red_stream;
-    QBA_HIP(hipEventRecord(ctx->list_done[sl], L.stream));
-    QBA_HIP(hipStreamWaitEvent(rs, ctx->list_done[sl], 0));
-    if (zflags & 1u) {
-      QBA_HIP(hipMemsetAsync(L.H, 0, sizeof(int64_t) * C::HB, rs));
-      QBA_HIP(hipMemsetAsync(L.C, 0, sizeof(int64_t) * C::CB, rs));
-      QBA_HIP(hipMemsetAsync(L.P, 0, sizeof(int64_t) * C::W, rs));
-    }
-    if ((zflags & 2u) && L.stats) QBA_HIP(hipMemsetAsync(L.stats, 0, sizeof(int64_t) * C::STATS, rs));
-  }
   const dim3 rgrid((C::NBP / 4 + 255) / 256, (grid + QBA_RED_ROWS - 1) / QBA_RED_ROWS);
-  hipLaunchKernelGGL(qba_k_reduce<NP>, rgrid, dim3(256), 0, rs, slab, grid, L.H, L.C, L.P, L.stats);
+  hipLaunchKernelGGL(qba_k_reduce<NP>, rgrid, dim3(256), 0, L.stream, slab, grid, L.H, L.C, L.P, L.stats);
   QBA_HIP(hipGetLastError());
-  if (async) {
-    QBA_HIP(hipEventRecord(ctx->red_done[sl], rs));
-    ctx->red_recorded[sl] = true;
-    ctx->next_slab = sl ^ 1;
-  }
   return QBA_OK;
 }
 

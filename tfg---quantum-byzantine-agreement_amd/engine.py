@@ -75,17 +75,6 @@ class Engine:
     def stream(self) -> C.c_void_p:
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def async_reduce(self, enable: bool = True) -> None:
-        """Overlap each counting call's slab reduction with the caller's next
-        launch (qba_async_reduce); results are complete after join_reduce()."""
-        call("qba_async_reduce", self.ctx, int(enable))
-
-    def join_reduce(self) -> None:
-        """Make the current stream wait for every overlapped reduction issued
-        so far (qba_join_reduce); required before reading the counts and at
-        the end of a hipGraph capture."""
-        call("qba_join_reduce", self.ctx, self.stream())
-
     # -- sizes --------------------------------------------------------------
     @staticmethod
     def sizes(n: int) -> Tuple[int, int]:
