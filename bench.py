@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--per-gpu", type=float, default=1.25e8, help="entries per GPU per step")
     ap.add_argument("--mode", choices=["fused", "split", "sample"], default="fused",
                     help="fused (the headline), split (sample then check), sample (diagnostic: no check)")
+    ap.add_argument("--layout", choices=["packed", "bytes"], default="packed",
+                    help="list rows as nibbles (qba_*_packed, the shipped hot path) or one byte per value")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -157,7 +159,8 @@ def headline(args):
     per = int(args.per_gpu)
     info = eng.prepare(n)
     first = rank * per  # weak scaling: rank r owns global entries [r*per, (r+1)*per)
-    lists = eng.alloc_lists(n, per)
+    packed = args.layout == "packed"
+    lists = eng.alloc_packed(n, per) if packed else eng.alloc_lists(n, per)
     _, _, _, total = dist_mod.count_layout(n)
     # N > 1: step i's count all-reduce runs asynchronously (RCCL's own stream)
     # while step i+1 samples into the other count buffer; a buffer is reused
@@ -174,7 +177,15 @@ def headline(args):
         if pending[b] is not None:
             pending[b].wait()
             pending[b] = None
-        if args.mode == "fused":
+        if packed:
+            if args.mode == "fused":
+                eng.sample_check_packed(n, args.seed, first, per, lists, counts[b])
+            elif args.mode == "sample":
+                eng.sample_packed(n, args.seed, first, per, lists)
+            else:
+                eng.sample_packed(n, args.seed, first, per, lists)
+                eng.check_counts_packed(lists, n, per, counts[b])
+        elif args.mode == "fused":
             eng.sample_check(n, args.seed, first, per, lists, counts[b])
         elif args.mode == "sample":
             eng.sample(n, args.seed, first, per, lists)
@@ -240,7 +251,8 @@ def headline(args):
     if tp.exists():
         tj = json.loads(tp.read_text())
         sha = _lib_sha16()
-        if tj.get("per_launch_entries") == per and tj.get("n") == n and tj.get("mode") == args.mode:
+        if tj.get("per_launch_entries") == per and tj.get("n") == n and tj.get("mode") == args.mode and \
+                tj.get("layout", "bytes") == args.layout:
             if tj.get("libqba_sha16") == sha:
                 traffic, traffic_note = tj.get("hbm_bytes_per_launch"), f"PMC FETCH+WRITE of this build ({sha})"
             else:
@@ -263,6 +275,8 @@ def headline(args):
                         f"{per:.3g} entries/GPU (sizeL={per * world:.3g} over {world} GPU)",
             "n_parties": n, "n_dishonest": args.dishonest, "entries_per_gpu": per,
             "sizeL": per * world, "mode": args.mode, "sampler": "closed" if info["closed"] else "tables",
+            "list_layout": "nibble rows: 4 bits per value, (n+1) x sizeL/2 bytes (qba_sample_check_packed)"
+                           if packed else "byte rows: (n+1) x sizeL bytes (qba_sample_check)",
             "parallelism": f"sizeL sharded over {world} GPU(s)" + (
                 ", one all-reduce of counts per step ("
                 + ("RCCL" if torch.distributed.get_backend() == "nccl" else torch.distributed.get_backend())
@@ -280,9 +294,10 @@ def headline(args):
             "traffic_gbs": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
             "traffic_frac": traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
             "traffic_source": traffic_note,
-            "note": "achieved/frac count the BASELINE's 24 B/entry (lists written + read back once); the fused "
-                    "kernel writes them once and never re-reads, so the bytes HBM really moves are "
-                    "traffic (traffic_gbs / traffic_frac)",
+            "note": "achieved/frac count the BASELINE's 24 B/entry (byte lists written + read back once); the "
+                    "fused kernel writes them once and never re-reads"
+                    + (", as nibble rows (6 B/entry at n=11)" if packed else "")
+                    + ", so the bytes HBM really moves are traffic (traffic_gbs / traffic_frac)",
         },
         "verification": {"q_entries": int(Pn.sum()), "offdiag_collisions": offdiag},
     }
@@ -348,9 +363,11 @@ def config1(args, eng):
     import torch
     n, count = 11, 1_000_000
     info = eng.prepare(n)
-    lists = eng.alloc_lists(n, count)
+    packed = args.layout == "packed"
+    lists = eng.alloc_packed(n, count) if packed else eng.alloc_lists(n, count)
     counts = eng.alloc_counts(n)
-    eng.sample_check(n, args.seed, 0, count, lists, counts)  # allocates scratch before capture
+    fused = eng.sample_check_packed if packed else eng.sample_check
+    fused(n, args.seed, 0, count, lists, counts)  # allocates scratch before capture
     torch.cuda.synchronize()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -358,7 +375,7 @@ def config1(args, eng):
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
             for _ in range(args.steps):
-                eng.sample_check(n, args.seed, 0, count, lists, counts)
+                fused(n, args.seed, 0, count, lists, counts)
     torch.cuda.synchronize()
     for _ in range(max(1, args.warmup)):
         g.replay()
@@ -380,7 +397,8 @@ def config1(args, eng):
                  f"({args.steps} steps in one hipGraph)",
                  {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": ach / HBM_PEAK_GBS, "traffic": None,
-                  "note": "12 MB of lists stay in the 256 MB Infinity Cache; launch-bound"}, extra)
+                  "note": ("6 MB of nibble-row" if packed else "12 MB of byte-row")
+                          + " lists stay in the 256 MB Infinity Cache; launch-bound"}, extra)
 
 
 def config3(args, eng, n_inst=4096, count=100_000):

@@ -24,6 +24,13 @@
  *     row g = measured group g (row 0 is what rank 1 calls Li, row 1 is Lc,
  *     row g>=2 is party g's list).  ld % 4 == 0 and the base
  *     pointer must be 4-byte aligned.
+ *   - Packed lists (the *_packed entry points) hold the same matrix as NIBBLE
+ *     rows: byte b of row g = value of column 2b (low nibble) | value of
+ *     column 2b+1 (high nibble) << 4, row stride `ld` >= (count+1)/2 bytes
+ *     (same alignment rules; a missing last column's nibble is 0).  Every
+ *     sampled value is < w <= 16, so nothing is lost; the fused hot path
+ *     writes half the bytes.  qba_lists_pack /
+ *     qba_lists_unpack convert between the two layouts.
  *   - Count tensors are int64:  H[u][g][x] (w x (n+1) x w),
  *     C[u][g][h] ((w x (n+1) x (n+1)), symmetric, diagonal = |P_u|),
  *     P[u] = |P_u| (w).  Only Q-correlated positions (L0[k] != L1[k],
@@ -143,6 +150,25 @@ QBA_API int qba_last_stats(qba_ctx *ctx, int64_t *out2_host);
 QBA_API int qba_sample_check(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
                      uint64_t count, uint8_t *lists_dev, uint64_t ld, int64_t *H_dev,
                      int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);
+
+/* The same three passes over packed (nibble-row) lists; counts identical to
+ * the byte-layout calls on the same entries.  qba_check_counts_packed cannot
+ * see a value > 15 (not representable); values in [w, 15] are caught as in
+ * qba_check_counts (qba_last_stats). */
+QBA_API int qba_sample_packed(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first, uint64_t count,
+                              uint8_t *packed_dev, uint64_t ld, qba_stream stream);
+QBA_API int qba_sample_check_packed(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
+                                    uint64_t count, uint8_t *packed_dev, uint64_t ld, int64_t *H_dev,
+                                    int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);
+QBA_API int qba_check_counts_packed(qba_ctx *ctx, int n_parties, const uint8_t *packed_dev, uint64_t count,
+                                    uint64_t ld, int64_t *H_dev, int64_t *C_dev, int64_t *P_dev,
+                                    int accumulate, qba_stream stream);
+/* Rows [0, rows) of `count` columns between the layouts.  pack: *bad_dev (may
+ * be NULL) receives how many values were > 15 (stored as value & 15). */
+QBA_API int qba_lists_pack(qba_ctx *ctx, const uint8_t *lists_dev, uint64_t ld, int rows, uint64_t count,
+                           uint8_t *packed_dev, uint64_t ldp, int64_t *bad_dev, qba_stream stream);
+QBA_API int qba_lists_unpack(qba_ctx *ctx, const uint8_t *packed_dev, uint64_t ldp, int rows, uint64_t count,
+                             uint8_t *lists_dev, uint64_t ld, qba_stream stream);
 
 /* Batched independent runs (BASELINE configs[3]: 4096 independent 7-party
  * instances per GPU).  Instance i uses Philox key seed_base + i over entries

@@ -1,0 +1,177 @@
+"""GPU parity of the nibble-row ("packed") list kernels -- qba_sample_packed,
+qba_sample_check_packed, qba_check_counts_packed, qba_lists_pack/unpack --
+against the C twin (oracle/sampler_ref.c) and the byte-layout kernels.
+
+Layout (include/qba.h): byte b of row g = value of column 2b | value of
+column 2b+1 << 4.  Lists and counts must be bit-identical to the byte layout's
+on the same entries; the cases follow test_gpu_kernels.py's (ragged tails,
+chunk and 2^33 splits, unaligned chunk starts, collisions, out-of-range
+values) plus the layout's own edges (odd counts, nothing written past the last
+byte)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib
+import tfg_oracle as orc
+from conftest import GOLDEN, sub
+
+pytestmark = pytest.mark.gpu
+
+
+def _unpack(p, count):
+    return sub("engine").unpack_nibbles(p.cpu().numpy(), count)
+
+
+def _ref(engine, n, seed, first, count):
+    info = engine.prepare(n)
+    return oracle_lib.sample(n, seed, first, count, info["notq"], info["q"], info["closed"])
+
+
+def _same_counts(c, ref):
+    H, C, P, _ = oracle_lib.counts(ref, n=ref.shape[0] - 1)
+    gH, gC, gP = c.numpy()
+    return np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+
+
+@pytest.mark.parametrize("n,first,count", [(1, 0, 1001), (2, 7, 999), (3, 0, 4096), (4, 1, 30_001),
+                                           (5, 3, 777), (6, 0, 30_000), (7, 1 << 33, 5003), (8, 2, 40_003),
+                                           (9, 5, 40_000), (10, 0, 50_001), (11, 0, 100_003),
+                                           (11, (1 << 40) + 5, 20_001), (12, 6, 9_999), (13, 99, 3000),
+                                           (14, 0, 12_345), (15, 1, 8191)])
+def test_packed_sample_and_counts_bit_exact(engine, n, first, count):
+    seed = 0x5EED ^ (n << 20)
+    ref = _ref(engine, n, seed, first, count)
+    p = engine.sample_packed(n, seed, first, count)
+    assert np.array_equal(_unpack(p, count), ref)
+    p2, c = engine.sample_check_packed(n, seed, first, count)
+    assert np.array_equal(_unpack(p2, count), ref)
+    assert _same_counts(c, ref)
+    assert _same_counts(engine.check_counts_packed(p2, n, count), ref)
+
+
+@pytest.mark.parametrize("count", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 15, 16, 17, 31, 4099, 4100, 8197])
+def test_packed_tiny_and_ragged(engine, count):
+    """Tails (partial quads, a lone low nibble) and nothing written past byte
+    (count + 1) // 2 of any row."""
+    n, seed, first = 11, 2024, 10
+    ref = _ref(engine, n, seed, first, count)
+    buf = torch.zeros((n + 1, 4096 + (count + 1) // 2 // 4096 * 4096), dtype=torch.uint8, device=engine.device)
+    p, c = engine.sample_check_packed(n, seed, first, count, packed=buf)
+    torch.cuda.synchronize()
+    assert np.array_equal(_unpack(p, count), ref)
+    host = buf.cpu().numpy()
+    nb = (count + 1) // 2
+    assert not host[:, nb:].any()
+    if count % 2:
+        assert not (host[:, nb - 1] >> 4).any()  # the missing column's nibble
+    assert _same_counts(c, ref)
+    assert _same_counts(engine.check_counts_packed(p, n, count), ref)
+
+
+@pytest.mark.parametrize("first", [999, 1000])
+def test_packed_chunked_and_unaligned_chunk_starts(monkeypatch, first):
+    """QBA_CHUNK_ENTRIES = 40004: every chunk after the first starts at byte
+    20002 * k, off the wide step's 4-byte alignment every other chunk, so the
+    one-quad (byte-store) step runs for the cut and the wide one after it."""
+    monkeypatch.setenv("QBA_CHUNK_ENTRIES", "40004")
+    eng = sub("engine").Engine(0)
+    try:
+        n, seed, count = 11, 31337, 160_021
+        ref = _ref(eng, n, seed, first, count)
+        p, c = eng.sample_check_packed(n, seed, first, count)
+        assert np.array_equal(_unpack(p, count), ref)
+        assert _same_counts(c, ref)
+        assert np.array_equal(_unpack(eng.sample_packed(n, seed, first, count), count), ref)
+        assert _same_counts(eng.check_counts_packed(p, n, count), ref)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("n,first,count", [(11, (1 << 33) - 4000, 12_008), (11, (1 << 33) - 4001, 12_008),
+                                           (11, (1 << 34) - 3, 20_001), (11, (1 << 34) - 6, 20_001),
+                                           (7, (3 << 33) - 8, 16), (7, (3 << 33) - 7, 16)])
+def test_packed_split_at_counter_word(engine, n, first, count):
+    """Even first: split at the 2^33 multiple (an even column); odd first: the
+    per-entry path, no split.  Both bit-exact."""
+    seed = 0xC0FFEE + n
+    ref = _ref(engine, n, seed, first, count)
+    p, c = engine.sample_check_packed(n, seed, first, count)
+    assert np.array_equal(_unpack(p, count), ref)
+    assert _same_counts(c, ref)
+
+
+def test_pack_unpack_roundtrip(engine):
+    n, count = 11, 50_001
+    rng = np.random.default_rng(3)
+    L = rng.integers(0, 16, (n + 1, count)).astype(np.uint8)
+    d = torch.zeros((n + 1, 53_248), dtype=torch.uint8, device=engine.device)
+    d[:, :count] = torch.from_numpy(L).to(engine.device)
+    p = engine.pack(d, n + 1, count)
+    assert np.array_equal(_unpack(p, count), L)
+    back = engine.unpack(p, n + 1, count)
+    assert np.array_equal(back[:, :count].cpu().numpy(), L)
+    d[3, 17] = 16
+    with pytest.raises(sub("_lib").QbaError):
+        engine.pack(d, n + 1, count)
+
+
+def test_packed_counts_on_fixture_lists(engine):
+    """Check-only over packed injected fixture lists (tampered / uniform ones with
+    collisions) vs the numpy restatement."""
+    arrays = np.load(GOLDEN / "protocol_lists.npz")
+    for name in arrays.files:
+        L = arrays[name]
+        n = L.shape[0] - 1
+        if L.max() > 15:
+            continue
+        d = torch.zeros((n + 1, (L.shape[1] + 63) // 64 * 64), dtype=torch.uint8, device=engine.device)
+        d[:, : L.shape[1]] = torch.from_numpy(L)
+        c = engine.check_counts_packed(engine.pack(d, n + 1, L.shape[1]), n, L.shape[1])
+        gH, gC, gP = c.numpy()
+        H, C, P = orc.counts(L, n)
+        assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P), name
+
+
+def test_packed_out_of_range_and_collisions(engine):
+    """n = 3 (w = 4): values in [w, 15] at Q entries are caught by the range
+    test (stats) exactly as in the byte layout; lists full of collisions take
+    the pair slow path."""
+    n, count = 3, 50_001
+    lists = engine.sample(n, 77, 0, count)
+    torch.cuda.synchronize()
+    L = lists[:, :count].cpu().numpy().copy()
+    rng = np.random.default_rng(n)
+    isq = np.nonzero(L[0] != L[1])[0]
+    for k in rng.choice(isq, 7, replace=False):
+        L[rng.integers(2, n + 1), k] = rng.integers(4, 16)
+    d = torch.zeros_like(lists)
+    d[:, :count] = torch.from_numpy(L)
+    c = engine.check_counts_packed(engine.pack(d, n + 1, count), n, count)
+    H, C, P, bad = oracle_lib.counts(L, n)
+    assert bad == engine.last_stats()[0] >= 7
+    gH, gC, gP = c.numpy()
+    assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+    n, count = 11, 30_001
+    L = rng.integers(0, 4, (n + 1, count)).astype(np.uint8)
+    d = torch.zeros((n + 1, 30_720), dtype=torch.uint8, device=engine.device)
+    d[:, :count] = torch.from_numpy(L).to(engine.device)
+    c = engine.check_counts_packed(engine.pack(d, n + 1, count), n, count)
+    H, C, P, bad = oracle_lib.counts(L, n)
+    gH, gC, gP = c.numpy()
+    assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+
+
+def test_packed_headline_size_equals_byte_layout(engine):
+    """The bench workload (n = 11, 1.25e8 entries): the packed fused pass writes
+    exactly the byte layout's lists (unpacked on the device) and its counts."""
+    n, seed, count = 11, 0x5EED, 125_000_000
+    engine.prepare(n)
+    lists, cb = engine.sample_check(n, seed, 0, count)
+    p, cp = engine.sample_check_packed(n, seed, 0, count)
+    u = engine.unpack(p, n + 1, count)
+    assert torch.equal(u[:, :count], lists[:, :count])
+    for a, b in zip(cb.numpy(), cp.numpy()):
+        assert np.array_equal(a, b)
+    del lists, u
+    torch.cuda.empty_cache()

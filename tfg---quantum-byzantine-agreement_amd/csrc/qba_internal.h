@@ -22,7 +22,7 @@
 // ---------------------------------------------------------------------------
 #if defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||            \
     defined(QBA_EXP_NOTABLE) || defined(QBA_EXP_CHEAPRNG) || defined(QBA_EXP_PADVALU) || defined(QBA_EXP_PADLDS) || defined(QBA_EXP_DESYNC) || \
-    defined(QBA_EXP_PACKSTORE) || defined(QBA_EXP_NQSEL) || defined(QBA_EXP_DISTFOLD) || defined(QBA_EXP_SMALLNARROW) || defined(QBA_EXP_NOATOMIC) ||          \
+    defined(QBA_EXP_PACKSTORE) || defined(QBA_EXP_SMALLNARROW) || defined(QBA_EXP_NOATOMIC) ||          \
     defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_INTERLEAVE) ||             \
     defined(QBA_EXP_GRID) || defined(QBA_EXP_NARROW) || defined(QBA_WIDE_QPT) || defined(QBA_MINW) || \
     defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) || defined(QBA_RED_ALL_IN_FLIGHT) ||           \

@@ -16,6 +16,7 @@ struct QbaLaunch {
   int accumulate;
   hipStream_t stream;
   int stats_accumulate;
+  int packed;  // nibble rows (qba.h "packed lists"): ld is the packed row stride in bytes
 };
 
 struct QbaBatch {

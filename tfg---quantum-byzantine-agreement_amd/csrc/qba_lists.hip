@@ -24,16 +24,18 @@ static int nbins_of(int n) {  // QCfg<n>::NBP
   return (w * g * (w + 1) + w * g * (g - 1) / 2 + 2 + 3) & ~3;
 }
 
+// packed: nibble rows, ld >= ceil(count / 2) bytes
 static int check_common(qba_ctx *ctx, int n, const uint8_t *lists, uint64_t count, uint64_t ld,
-                        const char *who) {
+                        const char *who, bool packed = false) {
   if (!ctx) return qba_fail(QBA_EINVAL, std::string(who) + ": ctx is NULL");
   if (n < 1 || n > QBA_MAX_PARTIES)
     return qba_fail(QBA_EUNSUPPORTED, std::string(who) + ": n_parties must be in [1, 15]");
   if (count == 0) return QBA_OK;
   if (!lists) return qba_fail(QBA_EINVAL, std::string(who) + ": lists is NULL");
-  if (ld < count || (ld & 3) || (reinterpret_cast<uintptr_t>(lists) & 3))
-    return qba_fail(QBA_EINVAL, std::string(who) +
-                                    ": need ld >= count, ld % 4 == 0 and a 4-byte aligned base");
+  const uint64_t need = packed ? (count + 1) / 2 : count;
+  if (ld < need || (ld & 3) || (reinterpret_cast<uintptr_t>(lists) & 3))
+    return qba_fail(QBA_EINVAL, std::string(who) + (packed ? ": need ld >= (count + 1) / 2" : ": need ld >= count") +
+                                    ", ld % 4 == 0 and a 4-byte aligned base");
   return qba_set_device(ctx);
 }
 
@@ -91,24 +93,35 @@ static int dispatch_one(qba_ctx *ctx, const QbaLaunch &L) {
 // that never cross a multiple of 2^33 entries (inside a launch the high word
 // of the Philox pair counter e >> 1 is constant: qba_sample_quad keeps it in
 // an SGPR); chunks after the first accumulate into the caller's counts.
+//
+// Nibble rows: every chunk boundary is an even column (whole bytes: chunk
+// sizes are multiples of 4, and an even first makes the 2^33 split even; an
+// odd first never takes the pair fast path, so it needs no split), so no
+// byte is shared by two launches.
 static int dispatch(qba_ctx *ctx, const QbaLaunch &L0) {
   QbaLaunch L = L0;
   uint64_t done = 0;
   int rc = QBA_OK;
   constexpr uint64_t PHI_SPAN = 1ull << 33;
+  const bool pk = L0.packed != 0;
+  const uintptr_t VA = pk ? 3 : 7;  // the wide step's row-vector alignment - 1
   do {
     L.count = L0.count - done < ctx->chunk ? L0.count - done : ctx->chunk;
-    const uint64_t to_span = PHI_SPAN - ((L0.first + done) & (PHI_SPAN - 1));
-    if (L.count > to_span) L.count = to_span;
-    // A chunk that starts off the wide kernels' 8-byte row alignment (the
-    // caller's first column, or the 2^33 split above when first % 8 != 0)
+    if (!pk || !((L0.first + done) & 1)) {
+      const uint64_t to_span = PHI_SPAN - ((L0.first + done) & (PHI_SPAN - 1));
+      if (L.count > to_span) L.count = to_span;
+    }
+    // A chunk that starts off the wide kernels' row alignment (8 B; 4 B for
+    // nibble rows) -- the caller's first column, or the 2^33 split above --
     // is cut to the next aligned column, so that every later chunk of the
     // call runs the wide kernel (qba_launch_lists picks the narrow one for
     // unaligned rows); rows must be aligned to begin with (ld % 8 == 0).
-    const uintptr_t mis = reinterpret_cast<uintptr_t>(L0.lists + done) & 7;
-    if (mis && !(L0.ld & 7) && L.count > 8 - mis) L.count = 8 - mis;
+    uint8_t *const at = L0.lists + (pk ? done >> 1 : done);
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(at) & VA;
+    const uint64_t cut = pk ? 2 * (4 - mis) : 8 - mis;
+    if (mis && !(L0.ld & VA) && L.count > cut) L.count = cut;
     L.first = L0.first + done;
-    L.lists = L0.lists + done;
+    L.lists = at;
     L.accumulate = done ? 1 : L0.accumulate;
     L.stats_accumulate = done ? 1 : 0;
     rc = dispatch_one(ctx, L);
@@ -158,6 +171,107 @@ extern "C" int qba_check_counts(qba_ctx *ctx, int n, const uint8_t *lists, uint6
   QbaLaunch L{n, 2, nullptr, 0, 0, count, const_cast<uint8_t *>(lists), ld,
               H, C, P, ctx->stats, accumulate, (hipStream_t)stream};
   return dispatch(ctx, L);
+}
+
+// ---- nibble rows ("packed lists", qba.h) ----------------------------------------
+extern "C" int qba_sample_packed(qba_ctx *ctx, int n, uint64_t seed, uint64_t first, uint64_t count,
+                                 uint8_t *packed, uint64_t ldp, qba_stream stream) {
+  int rc = check_common(ctx, n, packed, count, ldp, "qba_sample_packed", true);
+  if (rc || count == 0) return rc;
+  if ((rc = need_program(ctx, n, "qba_sample_packed"))) return rc;
+  QbaLaunch L{n, 0, (const QbaProgramSet *)ctx->prog_dev[n], seed, first, count, packed, ldp,
+              nullptr, nullptr, nullptr, nullptr, 0, (hipStream_t)stream, 0, 1};
+  return dispatch(ctx, L);
+}
+
+extern "C" int qba_sample_check_packed(qba_ctx *ctx, int n, uint64_t seed, uint64_t first,
+                                       uint64_t count, uint8_t *packed, uint64_t ldp, int64_t *H,
+                                       int64_t *C, int64_t *P, int accumulate, qba_stream stream) {
+  int rc = check_common(ctx, n, packed, count, ldp, "qba_sample_check_packed", true);
+  if (rc) return rc;
+  if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_sample_check_packed: H, C and P are required");
+  if (count == 0) return accumulate ? QBA_OK : zero_counts(n, H, C, P, (hipStream_t)stream);
+  if ((rc = need_program(ctx, n, "qba_sample_check_packed"))) return rc;
+  QbaLaunch L{n, 1, (const QbaProgramSet *)ctx->prog_dev[n], seed, first, count, packed, ldp,
+              H, C, P, ctx->stats, accumulate, (hipStream_t)stream, 0, 1};
+  return dispatch(ctx, L);
+}
+
+extern "C" int qba_check_counts_packed(qba_ctx *ctx, int n, const uint8_t *packed, uint64_t count,
+                                       uint64_t ldp, int64_t *H, int64_t *C, int64_t *P, int accumulate,
+                                       qba_stream stream) {
+  int rc = check_common(ctx, n, packed, count, ldp, "qba_check_counts_packed", true);
+  if (rc) return rc;
+  if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_check_counts_packed: H, C and P are required");
+  if (count == 0) return accumulate ? QBA_OK : zero_counts(n, H, C, P, (hipStream_t)stream);
+  QbaLaunch L{n, 2, nullptr, 0, 0, count, const_cast<uint8_t *>(packed), ldp,
+              H, C, P, ctx->stats, accumulate, (hipStream_t)stream, 0, 1};
+  return dispatch(ctx, L);
+}
+
+// Byte rows <-> nibble rows, one packed byte per thread (conversion helpers,
+// not on the hot path).  bad counts values > 15 (not representable; their
+// nibble is stored as value & 15).
+__global__ void qba_k_pack(const uint8_t *__restrict__ lists, uint64_t ld, uint64_t count, uint64_t nbytes,
+                           uint64_t total, uint8_t *__restrict__ packed, uint64_t ldp,
+                           unsigned long long *__restrict__ bad) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t g = t / nbytes, b = t - g * nbytes, c = 2 * b;
+    const uint8_t *r = lists + g * ld;
+    const uint32_t lo = r[c], hi = c + 1 < count ? r[c + 1] : 0u;
+    if (bad && (lo > 15u || hi > 15u)) atomicAdd(bad, (unsigned long long)((lo > 15u) + (hi > 15u)));
+    packed[g * ldp + b] = (uint8_t)((lo & 15u) | ((hi & 15u) << 4));
+  }
+}
+
+__global__ void qba_k_unpack(const uint8_t *__restrict__ packed, uint64_t ldp, uint64_t count, uint64_t nbytes,
+                             uint64_t total, uint8_t *__restrict__ lists, uint64_t ld) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t g = t / nbytes, b = t - g * nbytes, c = 2 * b;
+    const uint32_t v = packed[g * ldp + b];
+    uint8_t *r = lists + g * ld;
+    r[c] = (uint8_t)(v & 15u);
+    if (c + 1 < count) r[c + 1] = (uint8_t)(v >> 4);
+  }
+}
+
+static int convert_args(qba_ctx *ctx, const void *a, const void *b, int rows, uint64_t count, uint64_t ld,
+                        uint64_t ldp, const char *who) {
+  if (!ctx || rows < 0 || (rows && count && (!a || !b)) || (rows && count && (ld < count || ldp < (count + 1) / 2)))
+    return qba_fail(QBA_EINVAL, std::string(who) + ": bad arguments (ld >= count, ldp >= (count + 1) / 2)");
+  return qba_set_device(ctx);
+}
+
+static dim3 convert_grid(uint64_t total) {
+  const uint64_t b = (total + 255) / 256;
+  return dim3((unsigned)(b < 65536 ? (b ? b : 1) : 65536));
+}
+
+extern "C" int qba_lists_pack(qba_ctx *ctx, const uint8_t *lists, uint64_t ld, int rows, uint64_t count,
+                              uint8_t *packed, uint64_t ldp, int64_t *bad_dev, qba_stream stream) {
+  int rc = convert_args(ctx, lists, packed, rows, count, ld, ldp, "qba_lists_pack");
+  if (rc) return rc;
+  if (bad_dev) QBA_HIP(hipMemsetAsync(bad_dev, 0, sizeof(int64_t), (hipStream_t)stream));
+  const uint64_t nbytes = (count + 1) / 2, total = (uint64_t)rows * nbytes;
+  if (total == 0) return QBA_OK;
+  hipLaunchKernelGGL(qba_k_pack, convert_grid(total), dim3(256), 0, (hipStream_t)stream, lists, ld, count, nbytes,
+                     total, packed, ldp, reinterpret_cast<unsigned long long *>(bad_dev));
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
+}
+
+extern "C" int qba_lists_unpack(qba_ctx *ctx, const uint8_t *packed, uint64_t ldp, int rows, uint64_t count,
+                                uint8_t *lists, uint64_t ld, qba_stream stream) {
+  int rc = convert_args(ctx, packed, lists, rows, count, ld, ldp, "qba_lists_unpack");
+  if (rc) return rc;
+  const uint64_t nbytes = (count + 1) / 2, total = (uint64_t)rows * nbytes;
+  if (total == 0) return QBA_OK;
+  hipLaunchKernelGGL(qba_k_unpack, convert_grid(total), dim3(256), 0, (hipStream_t)stream, packed, ldp, count,
+                     nbytes, total, lists, ld);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
 }
 
 extern "C" int qba_reserve(qba_ctx *ctx, int n, int64_t max_blocks) {

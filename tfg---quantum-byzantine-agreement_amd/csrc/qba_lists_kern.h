@@ -264,10 +264,7 @@ __device__ __forceinline__ bool qba_accept(uint32_t F, uint32_t T) {
 // table reads are issued together: qba_closed_rank (not-Q words, Lemire rank;
 // (p, h) identify the entry for the rare retry) then qba_closed_finish.
 struct QbaClosed {
-  uint32_t nq[4];
-#ifdef QBA_EXP_NQSEL
-  uint32_t nqr[4];  // not-Q words before the nibble mask
-#endif
+  uint32_t nqr[4];  // not-Q words before the nibble mask (word 0 already masked)
   uint32_t rank, w0;
 };
 
@@ -279,16 +276,10 @@ __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64
   // nibbles) in byte order, group 0 = group 1: the masked words ARE the byte
   // layout, one v_perm in all (w0's low nibbles carry isQ and r)
   const uint32_t a = w1 & F::M4;
-  c.nq[0] = qba_perm_b(a, a, 0x03020101u);
-  c.nq[1] = (w1 >> 4) & F::M4;
-  c.nq[2] = (w0 >> 4) & F::M4;
-  c.nq[3] = 0u;
-#ifdef QBA_EXP_NQSEL
-  c.nqr[0] = c.nq[0];
+  c.nqr[0] = qba_perm_b(a, a, 0x03020101u);
   c.nqr[1] = w1 >> 4;
   c.nqr[2] = w0 >> 4;
   c.nqr[3] = 0u;
-#endif
   c.w0 = w0;
   const bool o1 = qba_accept<NP>(w1, F::T32);
   uint32_t rank = o1 ? w1 : (w0 & ~31u);
@@ -330,7 +321,8 @@ __device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint
   // for a mask plus a v_cndmask per word
   uint32_t qm = (uint32_t)__builtin_amdgcn_sbfe((int)c.w0, 0, 1);
   asm("" : "+v"(qm));
-#ifdef QBA_EXP_NQSEL  // experiment builds: not-Q words masked by one shared ~qm & M4 (and_or per word)
+  // not-Q words masked by ONE shared ~qm & M4, then one v_and_or per word:
+  // D = (nq_raw & nqm) | (qm & (q ^ R))  (-0.2 VALU/entry, profiles/r3/ab32)
   uint32_t nqm = ~qm & F::M4;
   asm("" : "+v"(nqm));
 #pragma unroll
@@ -339,10 +331,6 @@ __device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint
     asm("" : "+v"(t));
     D[i] = (c.nqr[i] & nqm) | t;
   }
-#else
-#pragma unroll
-  for (int i = 0; i < F::ND; ++i) D[i] = (qm & (q[i] ^ R)) | (~qm & c.nq[i]);
-#endif
 }
 
 // Stage table indices of a rank and the LDS reads.
@@ -528,16 +516,12 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
     if (4 * i + 3 < C::G) mq |= 0xffff0000u;
     U |= (qba_pk_onehot(D[i], one) & mp) | (qba_pk_onehot(D[i] >> 8, one) & mq);
   }
-#ifdef QBA_EXP_DISTFOLD  // experiment builds: lo | hi in one SDWA op (upper half zeroed)
-  {
+  {  // lo | hi in ONE op: an SDWA or with the upper half zeroed (was lshr + and_or)
     uint32_t r;
     asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
         : "=v"(r) : "v"(U));
     U = r;
   }
-#else
-  U = (U | (U >> 16)) & 0xffffu;
-#endif
   if (__popc(U) != C::G) {  // some pair collides: exact slow path
     // a compact loop (values picked by selects, no private array): this
     // path is rare and unrolling it would multiply the kernel's code size
@@ -875,6 +859,156 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
   }
 }
 
+// The same thread-step over NIBBLE rows (qba.h, "packed lists"): byte b of
+// row g holds columns 2b (low nibble) and 2b+1 (high nibble), half the bytes
+// of the byte layout.  Every value is < w <= 16, so two entries' byte-layout
+// words fold into one word -- D[2p] | D[2p+1] << 4, byte g' = the packed pair
+// of group 4i+g' -- BEFORE the transpose: one 4x4 transpose per 8 entries
+// (QPT = 2, one 4-B store per row) instead of two, and half the HBM writes,
+// which keeps the chip's clock up in the driver's cold window
+// (profiles/r3/ab32: 12-row packed stores 375-381 us vs 421-424 us).
+// QPT = 1 (unaligned starts, the tail quads): 2 bytes per row, stored as bytes
+// (a chunk may start at an odd byte).  MODE 2 reads the same layout; an
+// unpacked quad's entries come out permuted (counting is order-free).
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL>
+__device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
+                                            uint32_t k1, const QbaProgramSet *__restrict__ ps,
+                                            const uint64_t *pat, const uint64_t *apat,
+                                            const uint64_t *thr, const uint32_t *pl,
+                                            uint8_t *__restrict__ lists, uint64_t ld, uint32_t *hist,
+                                            QbaWaveQ *wq, bool act) {
+  using C = QCfg<NP>;
+  constexpr int ND = CF<NP>::ND;
+  static_assert(QPT == 1 || QPT == 2, "packed rows: QPT 1 or 2");
+  static_assert(!TAIL || QPT == 1, "tail quads are single");
+  static_assert(C::W <= 16, "a value must fit a nibble");
+  typedef __attribute__((address_space(1))) uint32_t GU;
+  const int valid = !TAIL ? 4 : ((count - c0) >= 4 ? 4 : (int)(count - c0));
+  const uint64_t cb = c0 >> 1;  // byte column of the step's first entry
+  uint32_t D[4][ND];
+  if constexpr (MODE == 2) {
+    uint32_t row[QPT][4 * ND];
+#pragma unroll
+    for (int k = 0; k < QPT; ++k)
+#pragma unroll
+      for (int g = 0; g < 4 * ND; ++g) row[k][g] = 0;
+    if (!TAIL && act) {
+#pragma unroll
+      for (int g = 0; g < C::G; ++g) {
+        if constexpr (QPT == 2) {
+          uint64_t rb = reinterpret_cast<uint64_t>(lists) + (uint64_t)g * ld;
+          asm("" : "+s"(rb));
+          const uint32_t v = __builtin_nontemporal_load(reinterpret_cast<const GU *>(rb + cb));
+          row[0][g] = v & 0x0f0f0f0fu;         // columns 0, 2, 4, 6
+          row[1][g] = (v >> 4) & 0x0f0f0f0fu;  // columns 1, 3, 5, 7
+        } else {
+          const uint8_t *r = lists + (uint64_t)g * ld + cb;
+          const uint32_t h = (uint32_t)r[0] | ((uint32_t)r[1] << 8);
+          row[0][g] = (h & 0x0f0fu) | ((h & 0xf0f0u) << 12);  // columns 0, 2, 1, 3
+        }
+      }
+    } else if (TAIL) {
+      for (int g = 0; g < C::G; ++g)
+        for (int j = 0; j < valid; ++j)
+          row[0][g] |= (uint32_t)((lists[(uint64_t)g * ld + cb + (j >> 1)] >> (4 * (j & 1))) & 15) << (8 * j);
+    }
+    const uint32_t am = act ? 0xffu : 0u;
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+        qba_t4(row[k][4 * i], row[k][4 * i + 1], row[k][4 * i + 2], row[k][4 * i + 3], D[0][i],
+               D[1][i], D[2][i], D[3][i]);
+      if (wq) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qba_q_push<NP, false>(*wq, D[j], qba_isq_d<NP>(D[j], am), hist);
+      } else {
+        qba_count_quad<NP>(D, TAIL ? valid : 4, hist, row[k]);
+      }
+    }
+  } else {
+    uint32_t Dp[2 * QPT][ND];  // pair p: entries 2p, 2p+1 of the step
+    const uint32_t am = act ? 0xffu : 0u;
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) {
+      qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        Dp[2 * k][i] = D[0][i] | (D[1][i] << 4);
+        Dp[2 * k + 1][i] = D[2][i] | (D[3][i] << 4);
+      }
+      if constexpr (MODE == 1) {
+        if (wq) {
+          // L0 != L1 (tfg.py:327) of a pair at once: nibble 0 / 1 of
+          // (byte 0 ^ byte 1) of its packed word 0 is entry 2p / 2p+1's test
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const uint32_t w0 = Dp[2 * k + p][0];
+            const uint32_t x = (w0 ^ (w0 >> 8)) & am;
+            qba_q_push<NP, true>(*wq, D[2 * p], (x & 0x0fu) != 0u, hist);
+            qba_q_push<NP, true>(*wq, D[2 * p + 1], x > 0x0fu, hist);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < valid) qba_count_d<NP>(D[j], 0x00010001u, hist, true);
+        }
+      }
+    }
+    if (!TAIL && act) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        uint32_t r[4];
+        if constexpr (QPT == 2)
+          qba_t4(Dp[0][i], Dp[1][i], Dp[2][i], Dp[3][i], r[0], r[1], r[2], r[3]);
+        else
+          qba_t4(Dp[0][i], Dp[1][i], 0u, 0u, r[0], r[1], r[2], r[3]);
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int g = 4 * i + gg;
+          if (g >= C::G) continue;
+          // row base opaque in SGPRs, 32-bit lane offset (as qba_step)
+          uint64_t rb = reinterpret_cast<uint64_t>(lists) + (uint64_t)g * ld;
+          asm("" : "+s"(rb));
+          if constexpr (QPT == 2) {
+#if QBA_NT_STORE
+            __builtin_nontemporal_store(r[gg], reinterpret_cast<GU *>(rb + cb));
+#else
+            *reinterpret_cast<GU *>(rb + cb) = r[gg];
+#endif
+          } else {
+            uint8_t *d = reinterpret_cast<uint8_t *>(rb + cb);
+            d[0] = (uint8_t)r[gg];
+            d[1] = (uint8_t)(r[gg] >> 8);
+          }
+        }
+      }
+    } else if (TAIL) {
+      // the call's last, partial quad: its bytes (a missing entry's nibble is 0)
+      for (int i = 0; i < ND; ++i)
+        for (int gg = 0; gg < 4; ++gg) {
+          const int g = 4 * i + gg;
+          if (g >= C::G) continue;
+          for (int b = 0; 2 * b < valid; ++b)
+            lists[(uint64_t)g * ld + cb + b] = (uint8_t)(Dp[b][i] >> (8 * gg));
+        }
+    }
+  }
+}
+
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, int PK>
+__device__ __forceinline__ void qba_step_l(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
+                                           uint32_t k1, const QbaProgramSet *__restrict__ ps,
+                                           const uint64_t *pat, const uint64_t *apat,
+                                           const uint64_t *thr, const uint32_t *pl,
+                                           uint8_t *__restrict__ lists, uint64_t ld, uint32_t *hist,
+                                           QbaWaveQ *wq = nullptr, bool act = true) {
+  if constexpr (PK)
+    qba_step_pk<NP, MODE, SAMP, QPT, TAIL>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
+  else
+    qba_step<NP, MODE, SAMP, QPT, TAIL>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
+}
+
 // Stage the program's tables in LDS; returns the histogram base after them.
 template <int NP, int MODE, int SAMP, int BS>
 __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__ ps, uint64_t *lds,
@@ -937,7 +1071,8 @@ __device__ __forceinline__ void qba_zero_outputs(const QbaZero &z, int tid, int 
 #else
 #define QBA_LISTS_BOUNDS __launch_bounds__(QBA_LBLOCK)
 #endif
-template <int NP, int MODE, int SAMP, int QPT>
+// PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row
+template <int NP, int MODE, int SAMP, int QPT, int PK>
 __global__ void QBA_LISTS_BOUNDS
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                 uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
@@ -996,13 +1131,13 @@ __global__ void QBA_LISTS_BOUNDS
     for (uint32_t u = u0;; u += ustride) {
       const bool act = u < nunits;
       if (!__any(act)) break;
-      qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
+      qba_step_l<NP, MODE, SAMP, QPT, false, PK>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
                                            lists, ld, hist, &wq, act);
     }
     while (wq.qn) qba_q_drain<NP, MODE == 1>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
   } else {
     for (uint32_t u = u0; u < nunits; u += ustride)
-      qba_step<NP, MODE, SAMP, QPT, false>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
+      qba_step_l<NP, MODE, SAMP, QPT, false, PK>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
                                            lists, ld, hist);
   }
   // the remaining < 4 QPT entries: whole quads, then the partial one
@@ -1010,9 +1145,9 @@ __global__ void QBA_LISTS_BOUNDS
   if (!(QBA_EXP_SKIP & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x < rq) {
     const uint32_t c0 = r0 + 4 * threadIdx.x;
     if (c0 + 4 <= count)
-      qba_step<NP, MODE, SAMP, 1, false>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
+      qba_step_l<NP, MODE, SAMP, 1, false, PK>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
     else
-      qba_step<NP, MODE, SAMP, 1, true>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
+      qba_step_l<NP, MODE, SAMP, 1, true, PK>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
   }
   if (MODE != 0) {
     __syncthreads();
@@ -1284,9 +1419,13 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
 #else
   const bool small = false;
 #endif
-  const bool wide = !small && !(reinterpret_cast<uintptr_t>(L.lists) & VA) && !(L.ld & VA);
+  // nibble rows: the wide step stores one 4-B word per row (QPT = 2)
+  const uintptr_t va = L.packed ? 3 : VA;
+  const bool wide = !small && !(reinterpret_cast<uintptr_t>(L.lists) & va) && !(L.ld & va);
 #endif
-#define QBA_K(M, S) (wide ? (const void *)qba_k_lists<NP, M, S, QBA_WIDE_QPT> : (const void *)qba_k_lists<NP, M, S, 1>)
+#define QBA_K(M, S)                                                                          \
+  (L.packed ? (wide ? (const void *)qba_k_lists<NP, M, S, 2, 1> : (const void *)qba_k_lists<NP, M, S, 1, 1>) \
+            : (wide ? (const void *)qba_k_lists<NP, M, S, QBA_WIDE_QPT, 0> : (const void *)qba_k_lists<NP, M, S, 1, 0>))
   const void *kern = nullptr;
   if (L.mode == 2) {
     kern = QBA_K(2, QBA_S_GENERAL);
@@ -1302,7 +1441,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   }
 #undef QBA_K
   if (lds > 65536) QBA_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const int grid = grid_for(ctx, kern, lds, L.count, wide ? QBA_GRID_QPT : 1);
+  const int grid = grid_for(ctx, kern, lds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1);
   uint32_t *slab = nullptr;
   if (L.mode != 0) {
     int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBP * sizeof(uint32_t));

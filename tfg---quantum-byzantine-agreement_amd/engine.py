@@ -145,6 +145,13 @@ class Engine:
         ld = max(4096, (count + 4095) // 4096 * 4096)
         return torch.empty((n + 1, ld), dtype=torch.uint8, device=self.device)
 
+    def alloc_packed(self, n: int, count: int) -> torch.Tensor:
+        """Nibble rows (qba.h "packed lists"): (count + 1) // 2 bytes per row,
+        rows 4 KiB-aligned like alloc_lists."""
+        nb = (count + 1) // 2
+        ld = max(4096, (nb + 4095) // 4096 * 4096)
+        return torch.empty((n + 1, ld), dtype=torch.uint8, device=self.device)
+
     def alloc_counts(self, n: int) -> Counts:
         _, w = self.sizes(n)
         z = lambda *s: torch.zeros(s, dtype=torch.int64, device=self.device)  # noqa: E731
@@ -157,6 +164,14 @@ class Engine:
         if lists.stride(1) != 1 or lists.shape[1] < count:
             raise QbaError("lists rows must be contiguous and hold `count` entries")
         return lists.stride(0)
+
+    @staticmethod
+    def _packed_ok(packed: torch.Tensor, rows: int, count: int) -> int:
+        if packed.dtype != torch.uint8 or packed.dim() != 2 or packed.shape[0] != rows:
+            raise QbaError(f"packed lists must be a uint8 [{rows}, ld] device tensor")
+        if packed.stride(1) != 1 or packed.shape[1] < (count + 1) // 2:
+            raise QbaError("packed rows must be contiguous and hold (count + 1) // 2 bytes")
+        return packed.stride(0)
 
     # -- (A3/A4) sampling ---------------------------------------------------------
     def sample(self, n: int, seed: int, first: int, count: int,
@@ -181,6 +196,31 @@ class Engine:
         call("qba_sample_check", self.ctx, n, seed, first, count, _ptr(lists), ld,
              _ptr(counts.H), _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
         return lists, counts
+
+    def sample_packed(self, n: int, seed: int, first: int, count: int,
+                      packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """sample() into nibble rows."""
+        self.prepare(n)
+        if packed is None:
+            packed = self.alloc_packed(n, count)
+        ld = self._packed_ok(packed, n + 1, count)
+        call("qba_sample_packed", self.ctx, n, seed, first, count, _ptr(packed), ld, self.stream())
+        return packed
+
+    def sample_check_packed(self, n: int, seed: int, first: int, count: int,
+                            packed: Optional[torch.Tensor] = None, counts: Optional[Counts] = None,
+                            accumulate: bool = False) -> Tuple[torch.Tensor, Counts]:
+        """The fused hot path writing nibble rows (half the bytes of
+        sample_check; same lists and counts)."""
+        self.prepare(n)
+        if packed is None:
+            packed = self.alloc_packed(n, count)
+        if counts is None:
+            counts = self.alloc_counts(n)
+        ld = self._packed_ok(packed, n + 1, count)
+        call("qba_sample_check_packed", self.ctx, n, seed, first, count, _ptr(packed), ld,
+             _ptr(counts.H), _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
+        return packed, counts
 
     def sample_check_batched(self, n: int, seed_base: int, n_inst: int, count: int,
                              lists: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Counts]:
@@ -214,6 +254,48 @@ class Engine:
              _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
         return counts
 
+    def check_counts_packed(self, packed: torch.Tensor, n: int, count: int,
+                            counts: Optional[Counts] = None, accumulate: bool = False) -> Counts:
+        self._check_n(n)
+        if counts is None:
+            counts = self.alloc_counts(n)
+        ld = self._packed_ok(packed, n + 1, count)
+        call("qba_check_counts_packed", self.ctx, n, _ptr(packed), count, ld, _ptr(counts.H),
+             _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
+        return counts
+
+    def pack(self, lists: torch.Tensor, rows: int, count: int,
+             packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Byte rows -> nibble rows on the device; raises when a value > 15."""
+        if lists.dtype != torch.uint8 or lists.dim() != 2 or lists.shape[0] < rows or \
+                lists.stride(1) != 1 or lists.shape[1] < count:
+            raise QbaError("lists must be a uint8 [>= rows, >= count] device tensor")
+        if packed is None:
+            nb = (count + 1) // 2
+            packed = torch.empty((rows, max(4096, (nb + 4095) // 4096 * 4096)), dtype=torch.uint8,
+                                 device=self.device)
+        ldp = self._packed_ok(packed, rows, count)
+        bad = torch.empty(1, dtype=torch.int64, device=self.device)
+        call("qba_lists_pack", self.ctx, _ptr(lists), lists.stride(0), rows, count, _ptr(packed), ldp,
+             _ptr(bad), self.stream())
+        if int(bad.item()):
+            raise QbaError(f"{int(bad.item())} values > 15 cannot be stored as nibbles")
+        return packed
+
+    def unpack(self, packed: torch.Tensor, rows: int, count: int,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Nibble rows -> byte rows [rows, ld] on the device."""
+        ldp = self._packed_ok(packed, rows, count)
+        if out is None:
+            out = torch.empty((rows, max(4096, (count + 4095) // 4096 * 4096)), dtype=torch.uint8,
+                              device=self.device)
+        if out.dtype != torch.uint8 or out.dim() != 2 or out.shape[0] < rows or out.stride(1) != 1 or \
+                out.shape[1] < count:
+            raise QbaError("out must be a uint8 [>= rows, >= count] device tensor")
+        call("qba_lists_unpack", self.ctx, _ptr(packed), ldp, rows, count, _ptr(out), out.stride(0),
+             self.stream())
+        return out
+
     def count_tables(self, n: int, sizeL: int, seed: int = 0, lists: Optional[np.ndarray] = None,
                      chunk: int = 1 << 27, first: int = 0, device_out: bool = False):
         """Flat int64 [H | C | P] over entries [first, first + sizeL): injected
@@ -235,10 +317,13 @@ class Engine:
             dev[:, :sizeL] = torch.from_numpy(arr).to(self.device)
             self.check_counts(dev, n, sizeL, counts)
         else:
-            buf = self.alloc_lists(n, min(chunk, max(sizeL, 1)))
+            # the lists are sampled, counted and dropped: nibble rows (half the
+            # bytes written)
+            chunk = max(8, chunk & ~7)
+            buf = self.alloc_packed(n, min(chunk, max(sizeL, 1)))
             for off in range(0, sizeL, chunk):
-                self.sample_check(n, seed, first + off, min(chunk, sizeL - off), buf, counts,
-                                  accumulate=off > 0)
+                self.sample_check_packed(n, seed, first + off, min(chunk, sizeL - off), buf, counts,
+                                         accumulate=off > 0)
         if sizeL and self.last_stats()[0] != 0:
             raise QbaError("lists hold values >= w at Q-correlated positions: count mode "
                            "cannot evaluate them (the reference never produces such lists)")
@@ -462,6 +547,15 @@ class Engine:
         out = torch.empty_like(d_ctr)
         call("qba_philox_dev", self.ctx, _ptr(d_ctr), len(ctr), int(key), _ptr(out), self.stream())
         return out.cpu().numpy().view(np.uint32)
+
+
+def unpack_nibbles(packed: np.ndarray, count: int) -> np.ndarray:
+    """Host view of nibble rows [rows, >= (count+1)//2] as byte rows [rows, count]."""
+    p = np.asarray(packed, dtype=np.uint8)
+    out = np.empty((p.shape[0], 2 * ((count + 1) // 2)), dtype=np.uint8)
+    out[:, 0::2] = p[:, :(count + 1) // 2] & 15
+    out[:, 1::2] = p[:, :(count + 1) // 2] >> 4
+    return out[:, :count]
 
 
 def alias_build(probs: Sequence[float]) -> Tuple[np.ndarray, np.ndarray]:

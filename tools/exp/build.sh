@@ -14,5 +14,5 @@ F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -fvisibility=hidden -munsafe-fp-at
 /opt/rocm/bin/hipcc $F -DQBA_INST_N=$N "$@" -c $src/qba_lists_inst.hip -o $out/${name}_n$N.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/$name.so $out/$name.o $out/${name}_n$N.o \
   $here/../_build/qba_ctx.o $here/../_build/qba_exact.o $here/../_build/qba_sv.o $here/../_build/qba_resource.o \
-  $here/../_build/qba_rccl.o $here/../_build/qba_plan.o -ldl
+  $here/../_build/qba_rccl.o $here/../_build/qba_plan.o $here/../_build/qba_host.o -ldl
 rm -f $out/$name.o $out/${name}_n$N.o
