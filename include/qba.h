@@ -179,6 +179,12 @@ QBA_API int qba_sample_check_batched(qba_ctx *ctx, int n_parties, uint64_t seed_
                                      uint64_t ld, uint64_t inst_stride, int64_t *H_dev,
                                      int64_t *C_dev, int64_t *P_dev, qba_stream stream);
 
+/* The same over nibble rows (ld, inst_stride in bytes of packed rows). */
+QBA_API int qba_sample_check_batched_packed(qba_ctx *ctx, int n_parties, uint64_t seed_base,
+                                            int64_t n_instances, uint64_t count, uint8_t *packed_dev,
+                                            uint64_t ld, uint64_t inst_stride, int64_t *H_dev,
+                                            int64_t *C_dev, int64_t *P_dev, qba_stream stream);
+
 /* ---- (A5-A8) checks, exact-order mode (bit-exact protocol parity) --------------- */
 /* isQCorrList = {k : Li[k] != Lc[k]} (tfg.py:327) as ascending indices.
  * *count_host receives the number found; at most `cap` are written. Synchronous. */

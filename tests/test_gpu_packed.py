@@ -175,3 +175,21 @@ def test_packed_headline_size_equals_byte_layout(engine):
         assert np.array_equal(a, b)
     del lists, u
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n,count", [(7, 3001), (7, 3000), (12, 777)])
+def test_packed_batched_instances(engine, n, count):
+    """Batched runs (configs[3] shape, scaled down) over nibble rows: instance i
+    == an ordinary run with key base + i, lists and counts, odd and even counts,
+    closed-form and table samplers."""
+    n_inst, base = 37, 1000
+    info = engine.prepare(n)
+    lists, c = engine.sample_check_batched(n, base, n_inst, count, packed=True)
+    torch.cuda.synchronize()
+    for i in (0, 1, 17, 36):
+        ref = oracle_lib.sample(n, base + i, 0, count, info["notq"], info["q"], info["closed"])
+        assert np.array_equal(_unpack(lists[i], count), ref)
+        H, C, P, bad = oracle_lib.counts(ref, n)
+        assert np.array_equal(c.H[i].cpu().numpy(), H)
+        assert np.array_equal(c.C[i].cpu().numpy(), C)
+        assert np.array_equal(c.P[i].cpu().numpy(), P)

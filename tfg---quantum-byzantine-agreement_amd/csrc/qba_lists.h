@@ -29,6 +29,7 @@ struct QbaBatch {
   uint64_t ld, inst_stride;
   int64_t *H, *C, *P;
   hipStream_t stream;
+  int packed;  // nibble rows: ld / inst_stride in bytes of packed rows
 };
 
 template <int NP>

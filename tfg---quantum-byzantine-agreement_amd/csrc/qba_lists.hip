@@ -46,20 +46,19 @@ static int need_program(qba_ctx *ctx, int n, const char *who) {
   return QBA_OK;
 }
 
-extern "C" int qba_sample_check_batched(qba_ctx *ctx, int n, uint64_t seed_base, int64_t n_inst,
-                                        uint64_t count, uint8_t *lists, uint64_t ld,
-                                        uint64_t inst_stride, int64_t *H, int64_t *C, int64_t *P,
-                                        qba_stream stream) {
-  int rc = check_common(ctx, n, lists, count, ld, "qba_sample_check_batched");
+static int batched(qba_ctx *ctx, int n, uint64_t seed_base, int64_t n_inst, uint64_t count, uint8_t *lists,
+                   uint64_t ld, uint64_t inst_stride, int64_t *H, int64_t *C, int64_t *P, qba_stream stream,
+                   bool packed, const char *who) {
+  int rc = check_common(ctx, n, lists, count, ld, who, packed);
   if (rc) return rc;
   if (n_inst < 0 || !H || !C || !P || (n_inst > 1 && inst_stride < (uint64_t)(n + 1) * ld) ||
       (inst_stride & 3) || count >= (1ull << 31))
-    return qba_fail(QBA_EINVAL, "qba_sample_check_batched: bad arguments (inst_stride >= (n+1)*ld, "
+    return qba_fail(QBA_EINVAL, std::string(who) + ": bad arguments (inst_stride >= (n+1)*ld, "
                                 "multiple of 4; count < 2^31)");
   if (n_inst == 0 || count == 0) return QBA_OK;
-  if ((rc = need_program(ctx, n, "qba_sample_check_batched"))) return rc;
+  if ((rc = need_program(ctx, n, who))) return rc;
   QbaBatch B{n, (const QbaProgramSet *)ctx->prog_dev[n], seed_base, n_inst, count, lists, ld,
-             inst_stride, H, C, P, (hipStream_t)stream};
+             inst_stride, H, C, P, (hipStream_t)stream, packed ? 1 : 0};
   switch (n) {
 #define QBA_CASE(k)                                                                     \
   case k:                                                                               \
@@ -72,6 +71,22 @@ extern "C" int qba_sample_check_batched(qba_ctx *ctx, int n, uint64_t seed_base,
     default:
       return qba_fail(QBA_EUNSUPPORTED, "n_parties must be in [1, 15]");
   }
+}
+
+extern "C" int qba_sample_check_batched(qba_ctx *ctx, int n, uint64_t seed_base, int64_t n_inst,
+                                        uint64_t count, uint8_t *lists, uint64_t ld,
+                                        uint64_t inst_stride, int64_t *H, int64_t *C, int64_t *P,
+                                        qba_stream stream) {
+  return batched(ctx, n, seed_base, n_inst, count, lists, ld, inst_stride, H, C, P, stream, false,
+                 "qba_sample_check_batched");
+}
+
+extern "C" int qba_sample_check_batched_packed(qba_ctx *ctx, int n, uint64_t seed_base, int64_t n_inst,
+                                               uint64_t count, uint8_t *packed, uint64_t ld,
+                                               uint64_t inst_stride, int64_t *H, int64_t *C, int64_t *P,
+                                               qba_stream stream) {
+  return batched(ctx, n, seed_base, n_inst, count, packed, ld, inst_stride, H, C, P, stream, true,
+                 "qba_sample_check_batched_packed");
 }
 
 static int dispatch_one(qba_ctx *ctx, const QbaLaunch &L) {

@@ -1180,7 +1180,7 @@ __global__ void QBA_LISTS_BOUNDS
 // run with Philox key seed_base + i over entries [0, count).  A workgroup
 // owns whole instances, so its LDS histogram IS the instance's final count
 // and is written out directly (no slab, no reduce launch).
-template <int NP, int SAMP, int QPT>
+template <int NP, int SAMP, int QPT, int PK>
 __global__ void __launch_bounds__(QBA_BLOCK)
     qba_k_batched(const QbaProgramSet *__restrict__ ps, uint64_t seed_base, int64_t n_inst,
                   uint64_t count, uint8_t *__restrict__ lists, uint64_t ld, uint64_t inst_stride,
@@ -1209,22 +1209,22 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     for (uint32_t u = threadIdx.x;; u += QBA_BLOCK) {  // wave-uniform trip count
       const bool act = u < nunits;
       if (!__any(act)) break;
-      qba_step<NP, 1, SAMP, QPT, false>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,
+      qba_step_l<NP, 1, SAMP, QPT, false, PK>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,
                                         hist, &wq, act);
     }
     while (wq.qn) qba_q_drain<NP, true>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
 #else
     for (uint32_t u = threadIdx.x; u < nunits; u += QBA_BLOCK)
-      qba_step<NP, 1, SAMP, QPT, false>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,
+      qba_step_l<NP, 1, SAMP, QPT, false, PK>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,
                                         hist);
 #endif
     const uint32_t r0 = nunits * (4 * QPT), rq = ((uint32_t)count - r0 + 3) >> 2;
     if (threadIdx.x < rq) {
       const uint32_t c0 = r0 + 4 * threadIdx.x;
       if (c0 + 4 <= (uint32_t)count)
-        qba_step<NP, 1, SAMP, 1, false>(c0, (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld, hist);
+        qba_step_l<NP, 1, SAMP, 1, false, PK>(c0, (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld, hist);
       else
-        qba_step<NP, 1, SAMP, 1, true>(c0, (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld, hist);
+        qba_step_l<NP, 1, SAMP, 1, true, PK>(c0, (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld, hist);
     }
     __syncthreads();
     int64_t *h = H + inst * C::HB, *c = Cc + inst * C::CB, *p = P + inst * C::W;
@@ -1476,8 +1476,9 @@ int qba_launch_batched(qba_ctx *ctx, const QbaBatch &B) {
   if (QBA_QUEUE) lds += (size_t)(QBA_BLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
   lds = (lds + 15) & ~(size_t)15;
   const int64_t cap = (int64_t)ctx->num_cus * 16;
-  // 8-B row vectors (two quads per thread-step) when every row start allows it
-  constexpr uintptr_t VA = 4 * QBA_WIDE_QPT - 1;
+  // 8-B row vectors (two quads per thread-step; 4 B for nibble rows) when
+  // every row start allows it
+  const uintptr_t VA = B.packed ? 3 : 4 * QBA_WIDE_QPT - 1;
   const bool wide = !(reinterpret_cast<uintptr_t>(B.lists) & VA) && !(B.ld & VA) && !(B.inst_stride & VA);
   const int grid = (int)(B.n_inst < cap ? B.n_inst : cap);
   auto go = [&](auto kern) -> int {
@@ -1489,13 +1490,15 @@ int qba_launch_batched(qba_ctx *ctx, const QbaBatch &B) {
     QBA_HIP(hipGetLastError());
     return QBA_OK;
   };
+#define QBA_B(S)                                                                                   \
+  (B.packed ? (wide ? go(qba_k_batched<NP, S, 2, 1>) : go(qba_k_batched<NP, S, 1, 1>))                    \
+            : (wide ? go(qba_k_batched<NP, S, QBA_WIDE_QPT, 0>) : go(qba_k_batched<NP, S, 1, 0>)))
   if (samp == QBA_S_CLOSED) {
-    if constexpr (NP <= QBA_CLOSED_MAX_N)
-      return wide ? go(qba_k_batched<NP, QBA_S_CLOSED, QBA_WIDE_QPT>) : go(qba_k_batched<NP, QBA_S_CLOSED, 1>);
+    if constexpr (NP <= QBA_CLOSED_MAX_N) return QBA_B(QBA_S_CLOSED);
     return qba_fail(QBA_EUNSUPPORTED, "closed form beyond n = 11");
   }
-  if (samp == QBA_S_FAST)
-    return wide ? go(qba_k_batched<NP, QBA_S_FAST, QBA_WIDE_QPT>) : go(qba_k_batched<NP, QBA_S_FAST, 1>);
-  return wide ? go(qba_k_batched<NP, QBA_S_GENERAL, QBA_WIDE_QPT>) : go(qba_k_batched<NP, QBA_S_GENERAL, 1>);
+  if (samp == QBA_S_FAST) return QBA_B(QBA_S_FAST);
+  return QBA_B(QBA_S_GENERAL);
+#undef QBA_B
 }
 

@@ -223,22 +223,28 @@ class Engine:
         return packed, counts
 
     def sample_check_batched(self, n: int, seed_base: int, n_inst: int, count: int,
-                             lists: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Counts]:
+                             lists: Optional[torch.Tensor] = None,
+                             packed: bool = False) -> Tuple[torch.Tensor, Counts]:
         """n_inst independent runs (key seed_base + i) of `count` entries each.
-        Returns lists [n_inst, n+1, ld] and per-instance counts [n_inst, ...]."""
+        Returns lists [n_inst, n+1, ld] (nibble rows when packed) and
+        per-instance counts [n_inst, ...]."""
         self.prepare(n)
         _, w = self.sizes(n)
         # rows start 4 KiB-aligned: the 8-B-per-lane row stores then never
         # straddle a partial line at a row start (1.3% over 64-B alignment at
         # n = 11, tools/exp/ldalign.sh)
-        ld = max(4096, (count + 4095) // 4096 * 4096)
+        nb = (count + 1) // 2 if packed else count
+        ld = max(4096, (nb + 4095) // 4096 * 4096)
         if lists is None:
             lists = torch.empty((n_inst, n + 1, ld), dtype=torch.uint8, device=self.device)
         if lists.dim() != 3 or lists.shape[:2] != (n_inst, n + 1) or lists.stride(2) != 1:
             raise QbaError("lists must be a uint8 [n_inst, n+1, ld] tensor")
         z = lambda *s: torch.empty(s, dtype=torch.int64, device=self.device)  # noqa: E731
         counts = Counts(z(n_inst, w, n + 1, w), z(n_inst, w, n + 1, n + 1), z(n_inst, w))
-        call("qba_sample_check_batched", self.ctx, n, seed_base, n_inst, count, _ptr(lists),
+        if lists.shape[2] < nb:
+            raise QbaError("lists rows too short for `count` entries")
+        call("qba_sample_check_batched_packed" if packed else "qba_sample_check_batched", self.ctx, n,
+             seed_base, n_inst, count, _ptr(lists),
              lists.stride(1), lists.stride(0), _ptr(counts.H), _ptr(counts.C), _ptr(counts.P),
              self.stream())
         return lists, counts

@@ -14,7 +14,7 @@ python $root/tools/trace_check.py $out/trace $out/trace_bench.json > $out/trace_
 bash $root/tools/pmc.sh gpurun_out/$tag/pmc
 python $root/tools/pmc_summary.py $out/pmc > $out/pmc_summary.txt
 python $root/tools/pmc_traffic.py $out/pmc 125000000 11 > $out/traffic_n11.json
-cp $out/traffic_n11.json $root/profiles/traffic_n11.json
+cp $out/traffic_n11.json $root/profiles/traffic_n11.json  # keyed to this build (bench.py checks the sha)
 cd $root
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench_driver.json 2> $out/bench_driver.err
 timeout -k 10 300 python -u -m tfg---quantum-byzantine-agreement_amd.tfg 1e9 3 --parties 11 --mode count --seed 11 --timing > $out/cli_count_1e9.txt 2>&1

@@ -8,7 +8,9 @@ gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts 64 B per
 for 16-B-per-lane stores and is calibrated here for the kernel's 4-B-per-lane
 row stores against the known list bytes written per launch ((n+1) B/entry).
 
-    python tools/pmc_traffic.py <pmc dir> <entries per launch> <n> [mode]
+    python tools/pmc_traffic.py <pmc dir> <entries per launch> <n> [mode] [layout]
+
+layout "packed" (default: bench.py's default) writes (n+1)/2 B/entry, "bytes" (n+1).
 """
 import csv
 import hashlib
@@ -20,6 +22,7 @@ from pathlib import Path
 
 root, per, n = Path(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 mode = sys.argv[4] if len(sys.argv) > 4 else "fused"
+layout = sys.argv[5] if len(sys.argv) > 5 else "packed"
 vals = {}
 for f in root.glob("p*/**/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
@@ -27,8 +30,8 @@ for f in root.glob("p*/**/*counter_collection.csv"):
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 fetch = statistics.median(vals["FETCH_SIZE"]) * 1024 * 2
 write = statistics.median(vals["WRITE_SIZE"]) * 1024
-known = (n + 1) * per
-out = {"n": n, "per_launch_entries": per, "mode": mode,
+known = (n + 1) * per // (2 if layout == "packed" else 1)
+out = {"n": n, "per_launch_entries": per, "mode": mode, "layout": layout,
        "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
        "write_calibration": {"known_list_bytes": known, "write_over_known": write / known},
        "algorithmic_bytes_per_launch": 2 * (n + 1) * per,
