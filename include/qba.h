@@ -195,6 +195,15 @@ QBA_API int qba_isq_indices(qba_ctx *ctx, const uint8_t *li_dev, const uint8_t *
  * Lc is read).  Synchronous. */
 QBA_API int qba_select_eq(qba_ctx *ctx, const int64_t *order_dev, int64_t m, const uint8_t *lc_dev,
                   uint64_t lc_len, int64_t v, int64_t *out_dev, int64_t *count_host, qba_stream stream);
+/* Host-pointer forms of the two (the protocol host's calls; synchronous):
+ * idx_host / out_host receive the selected indices.  Inputs of at most 16384
+ * items run as ONE single-workgroup launch through zero-copy pinned staging
+ * (no copies), larger ones through the device compaction and one D2H. */
+QBA_API int qba_isq_indices_host(qba_ctx *ctx, const uint8_t *li_dev, const uint8_t *lc_dev, uint64_t count,
+                                 int64_t *idx_host, int64_t cap, int64_t *count_host, qba_stream stream);
+QBA_API int qba_select_eq_host(qba_ctx *ctx, const int64_t *order_host, int64_t m, const uint8_t *lc_dev,
+                               uint64_t lc_len, int64_t v, int64_t *out_host, int64_t *count_host,
+                               qba_stream stream);
 /* tuple(Li[j] for j in P) in the given order (tfg.py:189, 291). */
 QBA_API int qba_gather(qba_ctx *ctx, const uint8_t *li_dev, uint64_t list_len, const int64_t *idx_dev,
                int64_t m, int64_t *out_dev, qba_stream stream);

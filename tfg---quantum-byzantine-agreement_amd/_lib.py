@@ -53,6 +53,8 @@ SIGNATURES = {
     "qba_sample_check_batched_packed": [_p, C.c_int, _u64, _i64, _u64, _p, _u64, _u64, _p, _p, _p, _p],
     "qba_isq_indices": [_p, _p, _p, _u64, _p, _i64, _pi64, _p],
     "qba_select_eq": [_p, _p, _i64, _p, _u64, _i64, _p, _pi64, _p],
+    "qba_isq_indices_host": [_p, _p, _p, _u64, _p, _i64, _pi64, _p],
+    "qba_select_eq_host": [_p, _p, _i64, _p, _u64, _i64, _p, _pi64, _p],
     "qba_check_gather": [_p, _p, C.c_uint64, C.c_int, C.c_uint64, _p, _p, _i64, _i64, _i64, _i64, _p, _p],
     "qba_check_packet": [_p, _p, _u64, _p, _i64, _i64, _i64, _i64, _p, _p],
     "qba_check_packet_host": [_p, _p, _u64, _p, _i64, _i64, _i64, _i64, _p, _p],

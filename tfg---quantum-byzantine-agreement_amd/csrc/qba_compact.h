@@ -95,6 +95,50 @@ __global__ void __launch_bounds__(QBA_CT_THREADS)
   }
 }
 
+// Inputs of at most QBA_CS_MAX items in ONE launch of one workgroup (the
+// exact-order protocol's small calls, e.g. configs[0]'s sizeL = 1000): the
+// predicate evaluated coalesced into LDS flags, 16 consecutive items ranked
+// per thread, the total written to *total by the last thread.  total and
+// whatever emit writes may be host memory (the zero-copy staging).
+#define QBA_CS_THREADS 1024
+#define QBA_CS_MAX (QBA_CS_THREADS * QBA_CT_ITEMS)
+template <class Pred>
+__global__ void __launch_bounds__(QBA_CS_THREADS)
+    qba_k_compact_small(Pred p, int64_t n, int64_t cap, int64_t *__restrict__ total) {
+  __shared__ int32_t wsum[QBA_CS_THREADS / 64];
+  __shared__ uint32_t flags[QBA_CS_MAX / 4];
+  uint8_t *f8 = reinterpret_cast<uint8_t *>(flags);
+  for (int r = 0; r < QBA_CT_ITEMS; ++r) {
+    const int64_t i = (int64_t)r * QBA_CS_THREADS + threadIdx.x;
+    f8[i] = (i < n && p.test(i)) ? 1 : 0;
+  }
+  __syncthreads();
+  const int64_t base = (int64_t)threadIdx.x * QBA_CT_ITEMS;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int q = 0; q < QBA_CT_ITEMS / 4; ++q)
+    bits |= ((flags[threadIdx.x * (QBA_CT_ITEMS / 4) + q] * 0x01020408u) >> 24) << (4 * q);
+  const int32_t c = __popc(bits);
+  int32_t incl = c;
+  const int lane = threadIdx.x & 63;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wsum[threadIdx.x >> 6] = incl;
+  __syncthreads();
+  int32_t wbase = 0;
+  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) wbase += wsum[w];
+  int64_t pos = wbase + incl - c;
+  if (threadIdx.x == QBA_CS_THREADS - 1) *total = pos + c;
+  while (bits) {
+    const int k = __ffs(bits) - 1;
+    bits &= bits - 1;
+    if (pos < cap) p.emit(base + k, pos);
+    ++pos;
+  }
+}
+
 // Runs the three passes on `stream`, then waits and returns the total in *count_host.
 template <class Pred>
 static int qba_compact(qba_ctx *ctx, Pred p, int64_t n, int64_t cap, int64_t *count_host,

@@ -69,6 +69,7 @@ extern "C" int qba_destroy(qba_ctx *ctx) {
   if (ctx->flag) (void)hipFree(ctx->flag);
   if (ctx->count1) (void)hipFree(ctx->count1);
   if (ctx->stats) (void)hipFree(ctx->stats);
+  if (ctx->zc) (void)hipHostFree(ctx->zc);
   if (ctx->pin_h) (void)hipHostFree(ctx->pin_h);
   if (ctx->pin_d) (void)hipFree(ctx->pin_d);
   delete ctx;
@@ -106,6 +107,23 @@ int qba_ensure_staging(qba_ctx *ctx, size_t host_bytes, size_t dev_bytes) {
     ctx->pin_h_bytes = sz;
   }
   return ensure(ctx->pin_d, ctx->pin_d_bytes, dev_bytes, "device staging");
+}
+
+int qba_ensure_zc(qba_ctx *ctx, size_t bytes) {
+  if (ctx->zc_bytes >= bytes) return QBA_OK;
+  if (ctx->zc) QBA_HIP(hipHostFree(ctx->zc));
+  ctx->zc = ctx->zc_d = nullptr;
+  ctx->zc_bytes = 0;
+  const size_t sz = bytes < 65536 ? 65536 : bytes + bytes / 4;
+  if (hipHostMalloc(&ctx->zc, sz, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return qba_fail(QBA_ENOMEM, "zero-copy staging allocation failed");
+  if (hipHostGetDevicePointer(&ctx->zc_d, ctx->zc, 0) != hipSuccess) {
+    (void)hipHostFree(ctx->zc);
+    ctx->zc = nullptr;
+    return qba_fail(QBA_EHIP, "zero-copy staging: no device address");
+  }
+  ctx->zc_bytes = sz;
+  return QBA_OK;
 }
 
 extern "C" int qba_last_stats(qba_ctx *ctx, int64_t *out2) {

@@ -160,6 +160,99 @@ extern "C" int qba_select_eq(qba_ctx *ctx, const int64_t *order, int64_t m, cons
   return QBA_OK;
 }
 
+// --- host-pointer forms (the protocol host's calls): small inputs in ONE
+// single-workgroup launch through the zero-copy staging, larger ones through
+// the device compaction and one D2H ---------------------------------------------------
+// the P filter over an order held in host memory: a bad index is a plain
+// store of 1 (no atomics on host memory)
+struct QbaSelPredZ {
+  const int64_t *order;
+  const uint8_t *lc;
+  uint64_t lc_len;
+  int64_t v;
+  int64_t *out;
+  int64_t *bad;
+  __device__ bool test(int64_t i) const {
+    const int64_t x = order[i];
+    if ((uint64_t)x >= lc_len) {
+      *bad = 1;
+      return false;
+    }
+    return (int64_t)lc[x] == v;
+  }
+  __device__ void emit(int64_t i, int64_t pos) const { out[pos] = order[i]; }
+};
+
+extern "C" int qba_isq_indices_host(qba_ctx *ctx, const uint8_t *li, const uint8_t *lc, uint64_t count,
+                                    int64_t *idx_host, int64_t cap, int64_t *count_host, qba_stream stream) {
+  if (!ctx || !count_host || (count && (!li || !lc)) || (cap > 0 && !idx_host) || cap < 0)
+    return qba_fail(QBA_EINVAL, "qba_isq_indices_host: bad arguments");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t keep = std::min<int64_t>(cap, (int64_t)count);
+  if (count <= QBA_CS_MAX) {
+    if ((rc = qba_ensure_zc(ctx, 8 * (size_t)(keep + 1)))) return rc;
+    int64_t *z = static_cast<int64_t *>(ctx->zc), *zd = static_cast<int64_t *>(ctx->zc_d);
+    z[0] = 0;
+    if (count) {
+      hipLaunchKernelGGL(qba_k_compact_small<QbaIsqPred>, dim3(1), dim3(QBA_CS_THREADS), 0, s,
+                         QbaIsqPred{li, lc, zd + 1}, (int64_t)count, keep, zd);
+      QBA_HIP(hipGetLastError());
+      QBA_HIP(hipStreamSynchronize(s));
+    }
+    *count_host = z[0];
+    memcpy(idx_host, z + 1, 8 * (size_t)std::min<int64_t>(z[0], keep));
+    return QBA_OK;
+  }
+  if ((rc = qba_ensure_staging(ctx, 8 * (size_t)keep, 8 * (size_t)keep))) return rc;
+  int64_t *d = static_cast<int64_t *>(ctx->pin_d);
+  if ((rc = qba_compact(ctx, QbaIsqPred{li, lc, d}, (int64_t)count, keep, count_host, s))) return rc;
+  const size_t got = (size_t)std::min<int64_t>(*count_host, keep);
+  QBA_HIP(hipMemcpyAsync(ctx->pin_h, d, 8 * got, hipMemcpyDeviceToHost, s));
+  QBA_HIP(hipStreamSynchronize(s));
+  memcpy(idx_host, ctx->pin_h, 8 * got);
+  return QBA_OK;
+}
+
+extern "C" int qba_select_eq_host(qba_ctx *ctx, const int64_t *order_host, int64_t m, const uint8_t *lc,
+                                  uint64_t lc_len, int64_t v, int64_t *out_host, int64_t *count_host,
+                                  qba_stream stream) {
+  if (!ctx || !count_host || m < 0 || (m && (!order_host || !lc || !out_host)))
+    return qba_fail(QBA_EINVAL, "qba_select_eq_host: bad arguments");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (m == 0) {
+    *count_host = 0;
+    return QBA_OK;
+  }
+  if (m <= QBA_CS_MAX) {
+    // [total | bad | order (m) | out (m)]
+    if ((rc = qba_ensure_zc(ctx, 8 * (size_t)(2 + 2 * m)))) return rc;
+    int64_t *z = static_cast<int64_t *>(ctx->zc), *zd = static_cast<int64_t *>(ctx->zc_d);
+    z[0] = z[1] = 0;
+    memcpy(z + 2, order_host, 8 * (size_t)m);
+    hipLaunchKernelGGL(qba_k_compact_small<QbaSelPredZ>, dim3(1), dim3(QBA_CS_THREADS), 0, s,
+                       QbaSelPredZ{zd + 2, lc, lc_len, v, zd + 2 + m, zd + 1}, m, m, zd);
+    QBA_HIP(hipGetLastError());
+    QBA_HIP(hipStreamSynchronize(s));
+    if (z[1]) return qba_fail(QBA_EINVAL, "qba_select_eq_host: index outside Lc");
+    *count_host = z[0];
+    memcpy(out_host, z + 2 + m, 8 * (size_t)z[0]);
+    return QBA_OK;
+  }
+  if ((rc = qba_ensure_staging(ctx, 8 * (size_t)m, 16 * (size_t)m))) return rc;
+  int64_t *d_order = static_cast<int64_t *>(ctx->pin_d), *d_out = d_order + m;
+  memcpy(ctx->pin_h, order_host, 8 * (size_t)m);
+  QBA_HIP(hipMemcpyAsync(d_order, ctx->pin_h, 8 * (size_t)m, hipMemcpyHostToDevice, s));
+  if ((rc = qba_select_eq(ctx, d_order, m, lc, lc_len, v, d_out, count_host, stream))) return rc;
+  QBA_HIP(hipMemcpyAsync(ctx->pin_h, d_out, 8 * (size_t)*count_host, hipMemcpyDeviceToHost, s));
+  QBA_HIP(hipStreamSynchronize(s));
+  memcpy(out_host, ctx->pin_h, 8 * (size_t)*count_host);
+  return QBA_OK;
+}
+
 // --- tuple(Li[j] for j in P)  (tfg.py:189, 291) --------------------------------------
 __global__ void qba_k_gather(const uint8_t *__restrict__ li, const int64_t *__restrict__ idx,
                              int64_t m, int64_t *__restrict__ out) {
@@ -375,9 +468,74 @@ extern "C" int qba_check_gather(qba_ctx *ctx, const uint8_t *lists, uint64_t ld,
   return QBA_OK;
 }
 
-// Synchronous host-pointer form (the protocol host's per-packet call): the
-// stage goes through the ctx's pinned staging, the result comes back to
-// out_host; one H2D, one launch, one D2H, one stream sync.
+// The same packet check as ONE workgroup whose stage and output live in the
+// zero-copy staging (host memory): its counters are LDS atomics and the
+// output is written with plain stores, so nothing but the launch and one sync
+// stands between the host and the answer.  m <= QBA_GATHER_MAXM.
+__global__ void __launch_bounds__(1024)
+    qba_k_check_packet_zc(const uint8_t *__restrict__ li, uint64_t list_len, const int64_t *__restrict__ stage,
+                          int64_t m, int64_t len, int64_t v, int64_t w, int64_t *__restrict__ out) {
+  __shared__ unsigned int fl[3];
+  __shared__ unsigned int eq[QBA_GATHER_MAXM];
+  if (threadIdx.x < 3) fl[threadIdx.x] = 0u;
+  if (threadIdx.x < QBA_GATHER_MAXM) eq[threadIdx.x] = 0u;
+  __syncthreads();
+  const int64_t *order = stage, *t = stage + len;
+  for (int64_t k = threadIdx.x; k < len; k += blockDim.x) {
+    const int64_t j = order[k];
+    int64_t own = -1;
+    if ((uint64_t)j >= list_len)
+      atomicOr(&fl[0], 1u);
+    else
+      own = li[j];
+    out[k] = own;
+    if (own < 0 || own > w || own == v) atomicOr(&fl[2], 1u);
+    bool good = true;
+    for (int64_t a = 0; a < m; ++a) {
+      const int64_t x = t[a * len + k];
+      if (x < 0 || x > w || x == v) good = false;
+      for (int64_t b = a + 1; b < m && good; ++b)
+        if (t[b * len + k] == x) good = false;
+      if (x == own) atomicAdd(&eq[a], 1u);
+    }
+    if (!good) atomicOr(&fl[1], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) out[len + threadIdx.x] = fl[threadIdx.x];
+  if (threadIdx.x < m) out[len + 3 + threadIdx.x] = eq[threadIdx.x];
+}
+
+// k packets [order | rows] concatenated in the zero-copy staging (stage_host
+// copied in), outputs after them; one launch per packet, one sync.
+static int check_packets_zc(qba_ctx *ctx, const uint8_t *li, uint64_t list_len, const int64_t *stage_host,
+                            const int64_t *desc, int64_t k, int64_t w, size_t nin, size_t nout,
+                            int64_t *out_host, hipStream_t s) {
+  int rc = qba_ensure_zc(ctx, 8 * (nin + nout));
+  if (rc) return rc;
+  int64_t *z = static_cast<int64_t *>(ctx->zc), *zd = static_cast<int64_t *>(ctx->zc_d);
+  if (nin) memcpy(z, stage_host, 8 * nin);
+  size_t oi = 0, oo = nin;
+  for (int64_t i = 0; i < k; ++i) {
+    const int64_t m = desc[3 * i], len = desc[3 * i + 1], v = desc[3 * i + 2];
+    if (len > 0) {
+      hipLaunchKernelGGL(qba_k_check_packet_zc, dim3(1), dim3(1024), 0, s, li, list_len, zd + oi, m, len, v, w,
+                         zd + oo);
+      QBA_HIP(hipGetLastError());
+    } else {
+      for (int64_t q = 0; q < 3 + m; ++q) z[oo + q] = 0;
+    }
+    oi += (size_t)len * (size_t)(m + 1);
+    oo += (size_t)(len + 3 + m);
+  }
+  QBA_HIP(hipStreamSynchronize(s));
+  memcpy(out_host, z + nin, 8 * nout);
+  return QBA_OK;
+}
+
+// Synchronous host-pointer form (the protocol host's per-packet call): a
+// small packet (m <= 64 tuples, <= QBA_ZC_MAX bytes) is checked by one
+// workgroup straight from and into the zero-copy staging; a larger one goes
+// through the ctx's pinned staging: one H2D, one launch, one D2H, one sync.
 extern "C" int qba_check_packet_host(qba_ctx *ctx, const uint8_t *li, uint64_t list_len,
                                      const int64_t *stage_host, int64_t m, int64_t len, int64_t v,
                                      int64_t w, int64_t *out_host, qba_stream stream) {
@@ -386,8 +544,12 @@ extern "C" int qba_check_packet_host(qba_ctx *ctx, const uint8_t *li, uint64_t l
   int rc = qba_set_device(ctx);
   if (rc) return rc;
   const size_t nin = (size_t)len * (size_t)(m + 1), nout = (size_t)(len + 3 + m);
-  if ((rc = qba_ensure_staging(ctx, 8 * (nin > nout ? nin : nout), 8 * (nin + nout)))) return rc;
   hipStream_t s = (hipStream_t)stream;
+  if (m <= QBA_GATHER_MAXM && 8 * (nin + nout) <= QBA_ZC_MAX) {
+    const int64_t desc[3] = {m, len, v};
+    return check_packets_zc(ctx, li, list_len, stage_host, desc, 1, w, nin, nout, out_host, s);
+  }
+  if ((rc = qba_ensure_staging(ctx, 8 * (nin > nout ? nin : nout), 8 * (nin + nout)))) return rc;
   int64_t *pin = static_cast<int64_t *>(ctx->pin_h), *d_in = static_cast<int64_t *>(ctx->pin_d),
           *d_out = d_in + nin;
   if (nin) {
@@ -412,17 +574,21 @@ extern "C" int qba_check_packets_host(qba_ctx *ctx, const uint8_t *li, uint64_t 
   if (!ctx || !desc || !out_host || k < 1 || !stage_host)
     return qba_fail(QBA_EINVAL, "qba_check_packets_host: bad arguments");
   size_t nin = 0, nout = 0;
+  bool small = true;
   for (int64_t i = 0; i < k; ++i) {
     const int64_t m = desc[3 * i], len = desc[3 * i + 1];
     if (m < 0 || len < 0 || (len && !li))
       return qba_fail(QBA_EINVAL, "qba_check_packets_host: bad packet descriptor");
     nin += (size_t)len * (size_t)(m + 1);
     nout += (size_t)(len + 3 + m);
+    small = small && m <= QBA_GATHER_MAXM;
   }
   int rc = qba_set_device(ctx);
   if (rc) return rc;
-  if ((rc = qba_ensure_staging(ctx, 8 * (nin > nout ? nin : nout), 8 * (nin + nout)))) return rc;
   hipStream_t s = (hipStream_t)stream;
+  if (small && 8 * (nin + nout) <= QBA_ZC_MAX)
+    return check_packets_zc(ctx, li, list_len, stage_host, desc, k, w, nin, nout, out_host, s);
+  if ((rc = qba_ensure_staging(ctx, 8 * (nin > nout ? nin : nout), 8 * (nin + nout)))) return rc;
   int64_t *pin = static_cast<int64_t *>(ctx->pin_h), *d_in = static_cast<int64_t *>(ctx->pin_d),
           *d_out = d_in + nin;
   if (nin) {
@@ -487,17 +653,18 @@ extern "C" int qba_lists_to_bits_host(qba_ctx *ctx, const uint8_t *lists, uint64
   if (n == 0) return QBA_OK;
   int rc = qba_set_device(ctx);
   if (rc) return rc;
-  if ((rc = qba_ensure_staging(ctx, 8 * n, 8 * n))) return rc;
   hipStream_t s = (hipStream_t)stream;
-  int64_t *d = static_cast<int64_t *>(ctx->pin_d);
+  const bool zc = 8 * n <= QBA_ZC_MAX;  // small: the kernels write the host staging directly
+  if ((rc = zc ? qba_ensure_zc(ctx, 8 * n) : qba_ensure_staging(ctx, 8 * n, 8 * n))) return rc;
+  int64_t *d = static_cast<int64_t *>(zc ? ctx->zc_d : ctx->pin_d);
   const unsigned grid = (unsigned)std::min<uint64_t>((count * nq + 255) / 256, 8192);
   for (int g = 0; g < rows; ++g)
     hipLaunchKernelGGL(qba_k_values_to_bits, dim3(grid), dim3(256), 0, s, lists + (uint64_t)g * ld, count, nq,
                        d + (size_t)g * count * nq);
   QBA_HIP(hipGetLastError());
-  QBA_HIP(hipMemcpyAsync(ctx->pin_h, d, 8 * n, hipMemcpyDeviceToHost, s));
+  if (!zc) QBA_HIP(hipMemcpyAsync(ctx->pin_h, d, 8 * n, hipMemcpyDeviceToHost, s));
   QBA_HIP(hipStreamSynchronize(s));
-  memcpy(raw_host, ctx->pin_h, 8 * n);
+  memcpy(raw_host, zc ? ctx->zc : ctx->pin_h, 8 * n);
   return QBA_OK;
 }
 
@@ -511,13 +678,21 @@ extern "C" int qba_bits_to_values_host(qba_ctx *ctx, const int64_t *raw_host, ui
   int rc = qba_set_device(ctx);
   if (rc) return rc;
   const size_t n = count * (size_t)nq;
-  if ((rc = qba_ensure_staging(ctx, 8 * n, 8 * n))) return rc;
   hipStream_t s = (hipStream_t)stream;
-  memcpy(ctx->pin_h, raw_host, 8 * n);
-  QBA_HIP(hipMemcpyAsync(ctx->pin_d, ctx->pin_h, 8 * n, hipMemcpyHostToDevice, s));
+  const bool zc = 8 * n <= QBA_ZC_MAX;  // small: the kernel reads the host staging directly
+  const int64_t *src;
+  if (zc) {
+    if ((rc = qba_ensure_zc(ctx, 8 * n))) return rc;
+    memcpy(ctx->zc, raw_host, 8 * n);
+    src = static_cast<const int64_t *>(ctx->zc_d);
+  } else {
+    if ((rc = qba_ensure_staging(ctx, 8 * n, 8 * n))) return rc;
+    memcpy(ctx->pin_h, raw_host, 8 * n);
+    QBA_HIP(hipMemcpyAsync(ctx->pin_d, ctx->pin_h, 8 * n, hipMemcpyHostToDevice, s));
+    src = static_cast<const int64_t *>(ctx->pin_d);
+  }
   const unsigned grid = (unsigned)std::min<uint64_t>((count + 255) / 256, 8192);
-  hipLaunchKernelGGL(qba_k_bits_to_values, dim3(grid), dim3(256), 0, s, static_cast<const int64_t *>(ctx->pin_d),
-                     count, nq, vals);
+  hipLaunchKernelGGL(qba_k_bits_to_values, dim3(grid), dim3(256), 0, s, src, count, nq, vals);
   QBA_HIP(hipGetLastError());
   QBA_HIP(hipStreamSynchronize(s));
   return QBA_OK;

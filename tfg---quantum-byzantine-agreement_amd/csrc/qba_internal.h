@@ -181,6 +181,9 @@ struct qba_ctx {
   int64_t *stats = nullptr;  // [2]: last counts launch: Q entries with a value >= w, spare
   uint64_t chunk = QBA_CHUNK;  // entries per list-kernel launch (env QBA_CHUNK_ENTRIES, tests)
   // pinned host + device staging of the synchronous *_host entry points
+  void *zc = nullptr;     // zero-copy staging: coherent pinned host memory the kernels read / write
+  void *zc_d = nullptr;   // its device address
+  size_t zc_bytes = 0;
   void *pin_h = nullptr;
   size_t pin_h_bytes = 0;
   void *pin_d = nullptr;
@@ -194,6 +197,12 @@ void qba_rccl_release(qba_ctx *ctx);
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes);
 int qba_ensure_scan(qba_ctx *ctx, size_t bytes);
 int qba_ensure_staging(qba_ctx *ctx, size_t host_bytes, size_t dev_bytes);
+// Small synchronous host-pointer calls (<= QBA_ZC_MAX bytes staged) skip the
+// H2D / D2H copies: their kernels read the input from and write the result to
+// ctx->zc (through ctx->zc_d) with plain loads and stores -- no atomics on
+// host memory.
+#define QBA_ZC_MAX (1u << 20)
+int qba_ensure_zc(qba_ctx *ctx, size_t bytes);
 int qba_set_device(qba_ctx *ctx);
 
 static inline int qba_nq(int n) {  // ceil(log2(n+1)), tfg.py:317

@@ -354,23 +354,23 @@ class Engine:
     def isq_indices(self, li: torch.Tensor, lc: torch.Tensor) -> np.ndarray:
         """Ascending {k : Li[k] != Lc[k]} (tfg.py:327)."""
         count = li.numel()
-        out = torch.empty(max(count, 1), dtype=torch.int64, device=self.device)
+        out = np.empty(max(count, 1), np.int64)
         found = C.c_int64()
-        call("qba_isq_indices", self.ctx, _ptr(li), _ptr(lc), count, _ptr(out), count,
+        call("qba_isq_indices_host", self.ctx, _ptr(li), _ptr(lc), count, out.ctypes.data, count,
              C.byref(found), self.stream())
-        return out[: found.value].cpu().numpy()
+        return out[: found.value]
 
     def select_eq(self, order: np.ndarray, lc: torch.Tensor, v: int) -> np.ndarray:
         """[x for x in order if Lc[x] == v], order kept (tfg.py:182)."""
         m = len(order)
         if m == 0:
             return np.zeros(0, np.int64)
-        d_order = self.to_device(np.asarray(order, dtype=np.int64))
-        out = torch.empty(m, dtype=torch.int64, device=self.device)
+        h_order = np.ascontiguousarray(order, dtype=np.int64)
+        out = np.empty(m, np.int64)
         found = C.c_int64()
-        call("qba_select_eq", self.ctx, _ptr(d_order), m, _ptr(lc), lc.numel(), int(v), _ptr(out),
-             C.byref(found), self.stream())
-        return out[: found.value].cpu().numpy()
+        call("qba_select_eq_host", self.ctx, h_order.ctypes.data, m, _ptr(lc), lc.numel(), int(v),
+             out.ctypes.data, C.byref(found), self.stream())
+        return out[: found.value]
 
     def gather(self, li: torch.Tensor, order: np.ndarray) -> np.ndarray:
         """Li[j] for j in order (tfg.py:189, 291)."""
