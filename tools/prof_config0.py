@@ -51,6 +51,15 @@ def main(runs=50):
     print(f"wall per run: {wall * 1e3:.3f} ms (instrumented {wall2 * 1e3:.3f} ms)")
     for k in sorted(te.t, key=te.t.get, reverse=True):
         print(f"  {k:18s} {te.n[k] / runs:6.1f} calls/run  {te.t[k] / runs * 1e3:7.3f} ms/run")
+    if "--cprofile" in sys.argv:  # where the host's own time goes (cProfile inflates it)
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for s in range(runs):
+            protocol.run_local(3, 1000, 1, eng, seed=1 + s)
+        pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(40)
     eng.close()
 
 
