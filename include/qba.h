@@ -274,7 +274,9 @@ QBA_API int qba_values_to_bits(qba_ctx *ctx, const uint8_t *values_dev, uint64_t
 QBA_API int qba_lists_to_bits_host(qba_ctx *ctx, const uint8_t *lists_dev, uint64_t ld, int rows,
                                    uint64_t count, int nq, int64_t *raw_host, qba_stream stream);
 /* measure_to_ints of a received row (tfg.py:158, 161) straight from the
- * receive buffer in host memory to a device list.  Synchronous. */
+ * receive buffer in host memory to a device list.  raw_host may be reused
+ * as soon as the call returns; the decode is ordered on `stream` (small rows
+ * are read from zero-copy staging without waiting; larger ones wait). */
 QBA_API int qba_bits_to_values_host(qba_ctx *ctx, const int64_t *raw_host, uint64_t count, int nq,
                                     uint8_t *values_dev, qba_stream stream);
 

@@ -69,6 +69,8 @@ extern "C" int qba_destroy(qba_ctx *ctx) {
   if (ctx->flag) (void)hipFree(ctx->flag);
   if (ctx->count1) (void)hipFree(ctx->count1);
   if (ctx->stats) (void)hipFree(ctx->stats);
+  if (ctx->zc_pending) (void)hipEventSynchronize(ctx->zc_ev);
+  if (ctx->zc_ev) (void)hipEventDestroy(ctx->zc_ev);
   if (ctx->zc) (void)hipHostFree(ctx->zc);
   if (ctx->pin_h) (void)hipHostFree(ctx->pin_h);
   if (ctx->pin_d) (void)hipFree(ctx->pin_d);
@@ -110,6 +112,10 @@ int qba_ensure_staging(qba_ctx *ctx, size_t host_bytes, size_t dev_bytes) {
 }
 
 int qba_ensure_zc(qba_ctx *ctx, size_t bytes) {
+  if (ctx->zc_pending) {  // an asynchronous kernel may still read the staging
+    QBA_HIP(hipEventSynchronize(ctx->zc_ev));
+    ctx->zc_pending = false;
+  }
   if (ctx->zc_bytes >= bytes) return QBA_OK;
   if (ctx->zc) QBA_HIP(hipHostFree(ctx->zc));
   ctx->zc = ctx->zc_d = nullptr;

@@ -693,6 +693,13 @@ extern "C" int qba_bits_to_values_host(qba_ctx *ctx, const int64_t *raw_host, ui
   }
   const unsigned grid = (unsigned)std::min<uint64_t>((count + 255) / 256, 8192);
   hipLaunchKernelGGL(qba_k_bits_to_values, dim3(grid), dim3(256), 0, s, src, count, nq, vals);
+  if (zc) {  // no wait: the next user of the staging waits for this event instead
+    QBA_HIP(hipGetLastError());
+    if (!ctx->zc_ev) QBA_HIP(hipEventCreateWithFlags(&ctx->zc_ev, hipEventDisableTiming));
+    QBA_HIP(hipEventRecord(ctx->zc_ev, s));
+    ctx->zc_pending = true;
+    return QBA_OK;
+  }
   QBA_HIP(hipGetLastError());
   QBA_HIP(hipStreamSynchronize(s));
   return QBA_OK;

@@ -20,7 +20,7 @@
 // qba_build_flags() reports which were compiled in (0 for a shipped build;
 // tests/test_oracle_golden.py asserts it).
 // ---------------------------------------------------------------------------
-#if defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||            \
+#if defined(QBA_EXP_GTAB) || defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||            \
     defined(QBA_EXP_NOTABLE) || defined(QBA_EXP_CHEAPRNG) || defined(QBA_EXP_PADVALU) || defined(QBA_EXP_PADLDS) || defined(QBA_EXP_DESYNC) || \
     defined(QBA_EXP_PACKSTORE) || defined(QBA_EXP_SMALLNARROW) || defined(QBA_EXP_NOATOMIC) ||          \
     defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_INTERLEAVE) ||             \
@@ -184,6 +184,8 @@ struct qba_ctx {
   void *zc = nullptr;     // zero-copy staging: coherent pinned host memory the kernels read / write
   void *zc_d = nullptr;   // its device address
   size_t zc_bytes = 0;
+  hipEvent_t zc_ev = nullptr;  // recorded after an asynchronous reader of zc (bits_to_values_host)
+  bool zc_pending = false;     // qba_ensure_zc waits for it before zc is rewritten
   void *pin_h = nullptr;
   size_t pin_h_bytes = 0;
   void *pin_d = nullptr;

@@ -357,6 +357,18 @@ __device__ __forceinline__ void qba_closed_tables(uint32_t rank, const uint32_t 
   A = make_uint4(iA, iA * 3u, iA * 5u, 0u);
   sB = make_uint2(iB, iB * 7u);
   sC = iC * 9u;
+#elif defined(QBA_EXP_GTAB)  // experiment builds: stage tables read from global memory (L1 / L2), not LDS
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(1))) const v4u GA4;
+  typedef __attribute__((address_space(1))) const v2u GA2;
+  typedef __attribute__((address_space(1))) const uint32_t GA1;
+  const uintptr_t gb = reinterpret_cast<uintptr_t>(pl);
+  const v4u a4 = *reinterpret_cast<GA4 *>(gb + 16 * (uintptr_t)iA);
+  const v2u b2 = *reinterpret_cast<GA2 *>(gb + 4 * (uintptr_t)(F::OFFB + 2 * iB));
+  A = make_uint4(a4.x, a4.y, a4.z, a4.w);
+  sB = make_uint2(b2.x, b2.y);
+  sC = F::RC > 1 ? *reinterpret_cast<GA1 *>(gb + 4 * (uintptr_t)(F::OFFC + iC)) : 0u;
 #else
   A = *reinterpret_cast<const uint4 *>(pl + 4 * iA);
   sB = *reinterpret_cast<const uint2 *>(pl + F::OFFB + 2 * iB);
@@ -1017,6 +1029,11 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   pat = apat = thr = lds;
   pl = reinterpret_cast<const uint32_t *>(lds);
   uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
+#ifdef QBA_EXP_GTAB
+  if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
+    pl = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
+  } else
+#endif
   if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
