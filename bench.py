@@ -359,7 +359,15 @@ def config0(args, eng):
 
 
 def config1(args, eng):
-    """configs[1]: n=11, sizeL=1e6 on one GPU; K steps in one hipGraph."""
+    """configs[1]: n=11, sizeL=1e6 on one GPU; K steps in one hipGraph.
+
+    The steps use the deferred reduction (qba_sample_check_packed_deferred,
+    include/qba.h): step k's count reduction runs in W workgroups of step
+    k+1's list kernel -- on CUs the 163 list workgroups leave idle -- instead
+    of a separate launch, and the graph ends with the flush of the last step,
+    so every step's counts are complete inside the timed replay.  The
+    synchronous form (list kernel + reduce launch per step) is timed beside it
+    (sync_us_per_step)."""
     import torch
     n, count = 11, 1_000_000
     info = eng.prepare(n)
@@ -367,29 +375,45 @@ def config1(args, eng):
     lists = eng.alloc_packed(n, count) if packed else eng.alloc_lists(n, count)
     counts = eng.alloc_counts(n)
     fused = eng.sample_check_packed if packed else eng.sample_check
-    fused(n, args.seed, 0, count, lists, counts)  # allocates scratch before capture
-    torch.cuda.synchronize()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(g, stream=s):
-            for _ in range(args.steps):
-                fused(n, args.seed, 0, count, lists, counts)
-    torch.cuda.synchronize()
-    for _ in range(max(1, args.warmup)):
+
+    def timed(deferred):
+        fused(n, args.seed, 0, count, lists, counts, deferred=deferred)  # allocates scratch before capture
+        fused(n, args.seed, 0, count, lists, counts, deferred=deferred)
+        eng.flush_deferred()
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(args.steps):
+                    fused(n, args.seed, 0, count, lists, counts, deferred=deferred)
+                if deferred:
+                    eng.flush_deferred()
+        torch.cuda.synchronize()
+        for _ in range(max(1, args.warmup)):
+            g.replay()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        t0 = time.perf_counter()
         g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / args.steps, a.elapsed_time(b) * 1e-3 / args.steps
+
+    sync_wall, sync_dev = timed(False)
+    wall, dev = timed(True)
+    # the verification result of the last step, checked against a synchronous pass
+    ref = eng.alloc_counts(n)
+    fused(n, args.seed, 0, count, lists, ref)
     torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    t0 = time.perf_counter()
-    g.replay()
-    b.record()
-    torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / args.steps
-    dev = a.elapsed_time(b) * 1e-3 / args.steps
+    same = all(torch.equal(x, y) for x, y in zip((counts.H, counts.C, counts.P), (ref.H, ref.C, ref.P)))
     ach = 24 * count / dev / 1e9
-    extra = {"ms_per_step": wall * 1e3}
+    extra = {"ms_per_step": wall * 1e3, "sync_us_per_step": sync_wall * 1e6,
+             "reduction": "deferred: step k's counts reduced inside step k+1's list kernel, the last by "
+                          "the flush at the end of the graph (qba_sample_check_packed_deferred)",
+             "verification": {"deferred_counts_equal_sync": bool(same)}}
     if not args.no_cpu_baseline:
         extra["cpu_baseline"] = cpu_baseline_counts(n, args.seed, info, args.cpu_seconds / 2)
     return _line(args, count / wall, "entries/s",

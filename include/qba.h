@@ -163,6 +163,24 @@ QBA_API int qba_sample_check_packed(qba_ctx *ctx, int n_parties, uint64_t seed, 
 QBA_API int qba_check_counts_packed(qba_ctx *ctx, int n_parties, const uint8_t *packed_dev, uint64_t count,
                                     uint64_t ld, int64_t *H_dev, int64_t *C_dev, int64_t *P_dev,
                                     int accumulate, qba_stream stream);
+/* Deferred reduction, for back-to-back count passes (BASELINE configs[1]:
+ * sizeL = 1e6 per pass, where the separate reduce launch is a third of the
+ * pass).  Same arguments and results as qba_sample_check / _packed (tfg.py:
+ * 68-84, 182, 189, 291-294, 327, consistent() 87-98), but the call's H, C, P
+ * and qba_last_stats are complete only after the NEXT deferred call on this
+ * ctx or qba_flush_deferred(ctx): the next call's list kernel reduces this
+ * call's slab rows in workgroups of its own (two alternating slab buffers).
+ * A call whose list workgroups fill the chip, any non-deferred counting call
+ * and qba_reserve flush the pending reduction first; a pending call on
+ * another stream is flushed there and ordered by an event. */
+QBA_API int qba_sample_check_deferred(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
+                                      uint64_t count, uint8_t *lists_dev, uint64_t ld, int64_t *H_dev,
+                                      int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);
+QBA_API int qba_sample_check_packed_deferred(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
+                                             uint64_t count, uint8_t *packed_dev, uint64_t ld, int64_t *H_dev,
+                                             int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);
+/* Launches the pending deferred reduction (if any) on its call's stream. */
+QBA_API int qba_flush_deferred(qba_ctx *ctx);
 /* Rows [0, rows) of `count` columns between the layouts.  pack: *bad_dev (may
  * be NULL) receives how many values were > 15 (stored as value & 15). */
 QBA_API int qba_lists_pack(qba_ctx *ctx, const uint8_t *lists_dev, uint64_t ld, int rows, uint64_t count,

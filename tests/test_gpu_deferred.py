@@ -1,0 +1,174 @@
+"""GPU parity of the deferred-reduction entry points (include/qba.h:
+qba_sample_check_deferred / qba_sample_check_packed_deferred /
+qba_flush_deferred).
+
+A deferred call's counts are reduced by the NEXT deferred call's list kernel
+(reduce workgroups ahead of its list workgroups, two alternating slab
+buffers) or by the flush, with plain stores of every output word.  The counts
+must be bit-identical to the synchronous calls' and to the C twin's, in every
+way a caller can chain them: separate outputs, one reused output buffer,
+accumulate, different n between calls, a synchronous call or an empty call in
+between, launches that fill the chip (the synchronous fallback), chunked
+calls, two streams, and a hipGraph replayed twice."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib
+from conftest import sub
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_counts(engine, n, seed, first, count):
+    info = engine.prepare(n)
+    ref = oracle_lib.sample(n, seed, first, count, info["notq"], info["q"], info["closed"])
+    H, C, P, _ = oracle_lib.counts(ref, n=n)
+    return H, C, P
+
+
+def _eq(c, ref):
+    gH, gC, gP = c.numpy()
+    return np.array_equal(gH, ref[0]) and np.array_equal(gC, ref[1]) and np.array_equal(gP, ref[2])
+
+
+def _call(engine, packed, n, seed, first, count, counts=None, accumulate=False, deferred=True):
+    f = engine.sample_check_packed if packed else engine.sample_check
+    return f(n, seed, first, count, counts=counts, accumulate=accumulate, deferred=deferred)[1]
+
+
+@pytest.mark.parametrize("packed", [True, False])
+@pytest.mark.parametrize("n", [1, 3, 7, 11, 13])
+def test_deferred_chain_separate_outputs(engine, packed, n):
+    """Four deferred calls into four output buffers, then the flush."""
+    calls = [(0x5EED + k, 1000 * k + (k & 1), 20_000 + 777 * k) for k in range(4)]
+    outs = [_call(engine, packed, n, s, f, c) for s, f, c in calls]
+    engine.flush_deferred()
+    torch.cuda.synchronize()
+    for (s, f, c), o in zip(calls, outs):
+        assert _eq(o, _ref_counts(engine, n, s, f, c)), (n, s, f, c)
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_deferred_reused_buffer_and_accumulate(engine, packed):
+    """configs[1]'s pattern: every pass into the same buffer (the last pass's
+    counts remain), then a run that accumulates its passes."""
+    n = 11
+    buf = engine.alloc_counts(n)
+    for k in range(5):
+        _call(engine, packed, n, 77, 50_000 * k, 1_000_000, counts=buf)
+    engine.flush_deferred()
+    torch.cuda.synchronize()
+    assert _eq(buf, _ref_counts(engine, n, 77, 200_000, 1_000_000))
+    acc = engine.alloc_counts(n)
+    parts = [(0, 30_001), (30_001, 12_000), (42_001, 99_999)]
+    for i, (f, c) in enumerate(parts):
+        _call(engine, packed, n, 9, f, c, counts=acc, accumulate=i > 0)
+    engine.flush_deferred()
+    torch.cuda.synchronize()
+    assert _eq(acc, _ref_counts(engine, n, 9, 0, 142_000))
+
+
+def test_deferred_mixed_with_sync_calls_and_n(engine):
+    """A pending reduction is flushed by a synchronous counting call, by an
+    empty call and by a deferred call of another n -- each into its own
+    outputs -- and a stale pending call never overwrites later results."""
+    a = _call(engine, True, 11, 1, 0, 40_000)
+    b = engine.sample_check_packed(11, 2, 0, 40_000)[1]          # synchronous: flushes a
+    c = _call(engine, True, 5, 3, 10, 30_000)
+    d = _call(engine, False, 11, 4, 0, 25_000)                   # other n: c reduced on its own
+    e = engine.alloc_counts(11)
+    _call(engine, True, 11, 5, 0, 0, counts=e)                   # empty: flushes d, zeroes e
+    f = _call(engine, True, 11, 6, 0, 33_333)
+    engine.check_counts_packed(engine.sample_packed(11, 7, 0, 1000), 11, 1000)  # flushes f
+    torch.cuda.synchronize()
+    assert _eq(a, _ref_counts(engine, 11, 1, 0, 40_000))
+    assert _eq(b, _ref_counts(engine, 11, 2, 0, 40_000))
+    assert _eq(c, _ref_counts(engine, 5, 3, 10, 30_000))
+    assert _eq(d, _ref_counts(engine, 11, 4, 0, 25_000))
+    assert not any(x.any() for x in (e.H.cpu(), e.C.cpu(), e.P.cpu()))
+    assert _eq(f, _ref_counts(engine, 11, 6, 0, 33_333))
+
+
+def test_deferred_full_chip_fallback_and_chunks(monkeypatch):
+    """A launch whose list workgroups fill every resident slot takes the
+    synchronous path (the pending call is flushed first); a chunked deferred
+    call defers chunk by chunk (each later chunk reduces the one before)."""
+    eng = sub("engine").Engine(0)
+    try:
+        n = 11
+        a = _call(eng, True, n, 41, 0, 50_000)
+        big = _call(eng, True, n, 42, 123, 12_000_000)  # > 512 workgroups' worth: fallback
+        b = _call(eng, True, n, 43, 0, 50_000)
+        eng.flush_deferred()
+        torch.cuda.synchronize()
+        assert _eq(a, _ref_counts(eng, n, 41, 0, 50_000))
+        assert _eq(big, _ref_counts(eng, n, 42, 123, 12_000_000))
+        assert _eq(b, _ref_counts(eng, n, 43, 0, 50_000))
+    finally:
+        eng.close()
+    monkeypatch.setenv("QBA_CHUNK_ENTRIES", "40004")
+    eng = sub("engine").Engine(0)
+    try:
+        c = _call(eng, True, 11, 44, 999, 160_021)
+        d = _call(eng, False, 11, 45, 1000, 120_013)
+        eng.flush_deferred()
+        torch.cuda.synchronize()
+        assert _eq(c, _ref_counts(eng, 11, 44, 999, 160_021))
+        assert _eq(d, _ref_counts(eng, 11, 45, 1000, 120_013))
+    finally:
+        eng.close()
+
+
+def test_deferred_two_streams(engine):
+    """A deferred call on another stream than the pending one: the pending
+    reduction is flushed on its own stream and the new stream waits for it
+    before reusing the slab."""
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for k in range(6):
+        with torch.cuda.stream(s1 if k % 2 == 0 else s2):
+            outs.append(_call(engine, True, 11, 100 + k, 0, 60_000 + k))
+    with torch.cuda.stream(s2):
+        engine.flush_deferred()
+    torch.cuda.synchronize()
+    for k, o in enumerate(outs):
+        assert _eq(o, _ref_counts(engine, 11, 100 + k, 0, 60_000 + k))
+
+
+def test_deferred_in_graph_replayed(engine):
+    """configs[1]'s bench form: K deferred passes + the flush captured in one
+    hipGraph; each replay reproduces the passes' counts."""
+    n, K = 11, 6
+    outs = [engine.alloc_counts(n) for _ in range(K)]
+    packed = engine.alloc_packed(n, 1_000_000)
+    for k in range(K):  # warm (programs, slab sizes) outside the capture
+        engine.sample_check_packed(n, 7 + k, k * 1_000_000, 1_000_000, packed, outs[k], deferred=True)
+    engine.flush_deferred()
+    torch.cuda.synchronize()
+    for o in outs:
+        for t in (o.H, o.C, o.P):
+            t.zero_()
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for k in range(K):
+                engine.sample_check_packed(n, 7 + k, k * 1_000_000, 1_000_000, packed, outs[k], deferred=True)
+            engine.flush_deferred()
+    for _ in range(2):
+        for o in outs:
+            for t in (o.H, o.C, o.P):
+                t.fill_(-1)
+        g.replay()
+        torch.cuda.synchronize()
+        for k, o in enumerate(outs):
+            assert _eq(o, _ref_counts(engine, n, 7 + k, k * 1_000_000, 1_000_000)), k
+
+
+def test_deferred_stats(engine):
+    """qba_last_stats after the flush is the stats of the last deferred call."""
+    _call(engine, True, 11, 5, 0, 10_000)
+    engine.flush_deferred()
+    torch.cuda.synchronize()
+    assert list(engine.last_stats()) == [0, 0]

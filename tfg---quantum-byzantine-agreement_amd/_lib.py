@@ -14,6 +14,8 @@ from pathlib import Path
 
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("QBA_LIB", _HERE / "_build" / "libqba.so"))
+# QBA_LIB naming a tools/exp/build.sh library (_build/exp/): an A/B build
+EXPERIMENT_LIB = LIB_PATH.parent.name == "exp"
 
 QBA_OK, QBA_EINVAL, QBA_EHIP, QBA_ENOMEM, QBA_EUNSUPPORTED, QBA_ESTATE = 0, -1, -2, -3, -4, -5
 KIND_NOTQ, KIND_Q = 0, 1
@@ -46,6 +48,9 @@ SIGNATURES = {
     "qba_sample_check": [_p, C.c_int, _u64, _u64, _u64, _p, _u64, _p, _p, _p, C.c_int, _p],
     "qba_sample_packed": [_p, C.c_int, _u64, _u64, _u64, _p, _u64, _p],
     "qba_sample_check_packed": [_p, C.c_int, _u64, _u64, _u64, _p, _u64, _p, _p, _p, C.c_int, _p],
+    "qba_sample_check_deferred": [_p, C.c_int, _u64, _u64, _u64, _p, _u64, _p, _p, _p, C.c_int, _p],
+    "qba_sample_check_packed_deferred": [_p, C.c_int, _u64, _u64, _u64, _p, _u64, _p, _p, _p, C.c_int, _p],
+    "qba_flush_deferred": [_p],
     "qba_check_counts_packed": [_p, C.c_int, _p, _u64, _u64, _p, _p, _p, C.c_int, _p],
     "qba_lists_pack": [_p, _p, _u64, C.c_int, _u64, _p, _u64, _p, _p],
     "qba_lists_unpack": [_p, _p, _u64, C.c_int, _u64, _p, _u64, _p],
@@ -98,6 +103,8 @@ def lib() -> C.CDLL:
                                QBA_ESTATE)
             handle = C.CDLL(str(LIB_PATH))
             for name, args in SIGNATURES.items():
+                if EXPERIMENT_LIB and not hasattr(handle, name):
+                    continue  # an A/B build of an older tree (tools/exp) may predate a symbol
                 fn = getattr(handle, name)
                 fn.argtypes = args
                 fn.restype = _RESTYPE.get(name, C.c_int)

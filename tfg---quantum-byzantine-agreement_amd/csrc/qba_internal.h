@@ -190,6 +190,16 @@ struct qba_ctx {
   size_t pin_h_bytes = 0;
   void *pin_d = nullptr;
   size_t pin_d_bytes = 0;
+  // the pending deferred reduction (qba_sample_check*_deferred): the slab rows
+  // of the last deferred call, reduced by the next one or qba_flush_deferred
+  struct {
+    int (*flush)(qba_ctx *ctx);  // per-n launcher of its reduction; null: none pending
+    const uint32_t *slab;
+    int rows, acc, sacc, buf;
+    int64_t *H, *C, *P, *stats;
+    hipStream_t stream;
+  } pend = {};
+  hipEvent_t def_ev = nullptr;  // orders a flush on one stream before slab reuse on another
   // RCCL communicator of the GPU-owner ranks (qba_rccl_init), or null
   void *rccl_comm = nullptr;
   int rccl_ranks = 0;

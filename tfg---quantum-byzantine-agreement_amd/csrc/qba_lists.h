@@ -17,6 +17,7 @@ struct QbaLaunch {
   hipStream_t stream;
   int stats_accumulate;
   int packed;  // nibble rows (qba.h "packed lists"): ld is the packed row stride in bytes
+  int defer;   // MODE 1: reduction deferred to the next deferred call / qba_flush_deferred
 };
 
 struct QbaBatch {
@@ -34,6 +35,9 @@ struct QbaBatch {
 
 template <int NP>
 int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L);
+// Launch the pending deferred reduction (if any) on its stream; a later launch
+// on stream `next` that reuses the slab then waits for it.
+int qba_flush_pending(qba_ctx *ctx, hipStream_t next);
 template <int NP>
 int qba_launch_batched(qba_ctx *ctx, const QbaBatch &B);
 // QBA_BUILD_EXPERIMENT_FLAGS of the per-n object (qba_build_flags ORs them)

@@ -145,7 +145,31 @@ static int dispatch(qba_ctx *ctx, const QbaLaunch &L0) {
   return rc;
 }
 
-static int zero_counts(int n, int64_t *H, int64_t *C, int64_t *P, hipStream_t s) {
+int qba_flush_pending(qba_ctx *ctx, hipStream_t next) {
+  auto &pd = ctx->pend;
+  if (!pd.flush) return QBA_OK;
+  int (*f)(qba_ctx *) = pd.flush;
+  int rc = f(ctx);
+  pd.flush = nullptr;
+  if (rc) return rc;
+  if (next != pd.stream) {  // the slab may be rewritten on `next`: after this reduction
+    if (!ctx->def_ev) QBA_HIP(hipEventCreateWithFlags(&ctx->def_ev, hipEventDisableTiming));
+    QBA_HIP(hipEventRecord(ctx->def_ev, pd.stream));
+    QBA_HIP(hipStreamWaitEvent(next, ctx->def_ev, 0));
+  }
+  return QBA_OK;
+}
+
+extern "C" int qba_flush_deferred(qba_ctx *ctx) {
+  if (!ctx) return qba_fail(QBA_EINVAL, "qba_flush_deferred: ctx is required");
+  if (!ctx->pend.flush) return QBA_OK;
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  return qba_flush_pending(ctx, ctx->pend.stream);
+}
+
+static int zero_counts(qba_ctx *ctx, int n, int64_t *H, int64_t *C, int64_t *P, hipStream_t s) {
+  if (int rc = qba_flush_pending(ctx, s)) return rc;  // a pending reduction may target the same outputs
   const int g = n + 1, w = 1 << qba_nq(n);
   QBA_HIP(hipMemsetAsync(H, 0, sizeof(int64_t) * w * g * w, s));
   QBA_HIP(hipMemsetAsync(C, 0, sizeof(int64_t) * w * g * g, s));
@@ -169,10 +193,25 @@ extern "C" int qba_sample_check(qba_ctx *ctx, int n, uint64_t seed, uint64_t fir
   int rc = check_common(ctx, n, lists, count, ld, "qba_sample_check");
   if (rc) return rc;
   if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_sample_check: H, C and P are required");
-  if (count == 0) return accumulate ? QBA_OK : zero_counts(n, H, C, P, (hipStream_t)stream);
+  if (count == 0)
+    return accumulate ? qba_flush_pending(ctx, (hipStream_t)stream) : zero_counts(ctx, n, H, C, P, (hipStream_t)stream);
   if ((rc = need_program(ctx, n, "qba_sample_check"))) return rc;
   QbaLaunch L{n, 1, (const QbaProgramSet *)ctx->prog_dev[n], seed, first, count, lists, ld,
               H, C, P, ctx->stats, accumulate, (hipStream_t)stream};
+  return dispatch(ctx, L);
+}
+
+extern "C" int qba_sample_check_deferred(qba_ctx *ctx, int n, uint64_t seed, uint64_t first,
+                                         uint64_t count, uint8_t *lists, uint64_t ld, int64_t *H,
+                                         int64_t *C, int64_t *P, int accumulate, qba_stream stream) {
+  int rc = check_common(ctx, n, lists, count, ld, "qba_sample_check_deferred");
+  if (rc) return rc;
+  if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_sample_check_deferred: H, C and P are required");
+  if (count == 0)
+    return accumulate ? qba_flush_pending(ctx, (hipStream_t)stream) : zero_counts(ctx, n, H, C, P, (hipStream_t)stream);
+  if ((rc = need_program(ctx, n, "qba_sample_check_deferred"))) return rc;
+  QbaLaunch L{n, 1, (const QbaProgramSet *)ctx->prog_dev[n], seed, first, count, lists, ld,
+              H, C, P, ctx->stats, accumulate, (hipStream_t)stream, 0, 0, 1};
   return dispatch(ctx, L);
 }
 
@@ -182,7 +221,8 @@ extern "C" int qba_check_counts(qba_ctx *ctx, int n, const uint8_t *lists, uint6
   int rc = check_common(ctx, n, lists, count, ld, "qba_check_counts");
   if (rc) return rc;
   if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_check_counts: H, C and P are required");
-  if (count == 0) return accumulate ? QBA_OK : zero_counts(n, H, C, P, (hipStream_t)stream);
+  if (count == 0)
+    return accumulate ? qba_flush_pending(ctx, (hipStream_t)stream) : zero_counts(ctx, n, H, C, P, (hipStream_t)stream);
   QbaLaunch L{n, 2, nullptr, 0, 0, count, const_cast<uint8_t *>(lists), ld,
               H, C, P, ctx->stats, accumulate, (hipStream_t)stream};
   return dispatch(ctx, L);
@@ -205,10 +245,25 @@ extern "C" int qba_sample_check_packed(qba_ctx *ctx, int n, uint64_t seed, uint6
   int rc = check_common(ctx, n, packed, count, ldp, "qba_sample_check_packed", true);
   if (rc) return rc;
   if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_sample_check_packed: H, C and P are required");
-  if (count == 0) return accumulate ? QBA_OK : zero_counts(n, H, C, P, (hipStream_t)stream);
+  if (count == 0)
+    return accumulate ? qba_flush_pending(ctx, (hipStream_t)stream) : zero_counts(ctx, n, H, C, P, (hipStream_t)stream);
   if ((rc = need_program(ctx, n, "qba_sample_check_packed"))) return rc;
   QbaLaunch L{n, 1, (const QbaProgramSet *)ctx->prog_dev[n], seed, first, count, packed, ldp,
               H, C, P, ctx->stats, accumulate, (hipStream_t)stream, 0, 1};
+  return dispatch(ctx, L);
+}
+
+extern "C" int qba_sample_check_packed_deferred(qba_ctx *ctx, int n, uint64_t seed, uint64_t first,
+                                                uint64_t count, uint8_t *packed, uint64_t ldp, int64_t *H,
+                                                int64_t *C, int64_t *P, int accumulate, qba_stream stream) {
+  int rc = check_common(ctx, n, packed, count, ldp, "qba_sample_check_packed_deferred", true);
+  if (rc) return rc;
+  if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_sample_check_packed_deferred: H, C and P are required");
+  if (count == 0)
+    return accumulate ? qba_flush_pending(ctx, (hipStream_t)stream) : zero_counts(ctx, n, H, C, P, (hipStream_t)stream);
+  if ((rc = need_program(ctx, n, "qba_sample_check_packed_deferred"))) return rc;
+  QbaLaunch L{n, 1, (const QbaProgramSet *)ctx->prog_dev[n], seed, first, count, packed, ldp,
+              H, C, P, ctx->stats, accumulate, (hipStream_t)stream, 0, 1, 1};
   return dispatch(ctx, L);
 }
 
@@ -218,7 +273,8 @@ extern "C" int qba_check_counts_packed(qba_ctx *ctx, int n, const uint8_t *packe
   int rc = check_common(ctx, n, packed, count, ldp, "qba_check_counts_packed", true);
   if (rc) return rc;
   if (!H || !C || !P) return qba_fail(QBA_EINVAL, "qba_check_counts_packed: H, C and P are required");
-  if (count == 0) return accumulate ? QBA_OK : zero_counts(n, H, C, P, (hipStream_t)stream);
+  if (count == 0)
+    return accumulate ? qba_flush_pending(ctx, (hipStream_t)stream) : zero_counts(ctx, n, H, C, P, (hipStream_t)stream);
   QbaLaunch L{n, 2, nullptr, 0, 0, count, const_cast<uint8_t *>(packed), ldp,
               H, C, P, ctx->stats, accumulate, (hipStream_t)stream, 0, 1};
   return dispatch(ctx, L);
@@ -294,6 +350,7 @@ extern "C" int qba_reserve(qba_ctx *ctx, int n, int64_t max_blocks) {
     return qba_fail(QBA_EINVAL, "qba_reserve: bad arguments");
   int rc = qba_set_device(ctx);
   if (rc) return rc;
+  if (ctx->pend.flush && (rc = qba_flush_pending(ctx, ctx->pend.stream))) return rc;  // before a reallocation
   return qba_ensure_slab(ctx, (size_t)max_blocks * nbins_of(n) * sizeof(uint32_t));
 }
 

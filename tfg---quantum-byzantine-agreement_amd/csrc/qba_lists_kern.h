@@ -1088,26 +1088,29 @@ __device__ __forceinline__ void qba_zero_outputs(const QbaZero &z, int tid, int 
 #else
 #define QBA_LISTS_BOUNDS __launch_bounds__(QBA_LBLOCK)
 #endif
-// PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row
+// PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row.
+// The body of the list kernel; its workgroups are those after the first
+// `red` (qba_k_lists: 0; qba_k_lists_def: its reduce workgroups).
 template <int NP, int MODE, int SAMP, int QPT, int PK>
-__global__ void QBA_LISTS_BOUNDS
-    qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
-                uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
-                uint32_t *__restrict__ slab, QbaZero zero) {
+__device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1,
+                                               uint64_t first, uint32_t count, uint8_t *__restrict__ lists,
+                                               uint64_t ld, uint32_t *__restrict__ slab, QbaZero zero,
+                                               uint32_t red) {
   using C = QCfg<NP>;
   constexpr int BS = QBA_LBLOCK;
   extern __shared__ __align__(16) uint64_t lds[];
+  const uint32_t bid = blockIdx.x - red, nblk = gridDim.x - red;
   const uint64_t *pat, *apat, *thr;
   const uint32_t *pl;
 #ifdef QBA_EXP_TIMING  // experiment builds: per-workgroup phase timestamps after the slab rows
-  uint64_t *tsl = reinterpret_cast<uint64_t *>(slab + (size_t)gridDim.x * C::NBP) + 8 * blockIdx.x;
+  uint64_t *tsl = reinterpret_cast<uint64_t *>(slab + (size_t)nblk * C::NBP) + 8 * bid;
   const uint64_t ts0 = wall_clock64();
 #endif
   uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
   if (MODE != 0) {
     for (int i = threadIdx.x; i < C::NBP; i += BS) hist[i] = 0u;
 #if !QBA_ZERO_AT_END
-    if (blockIdx.x == 0) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
+    if (bid == 0) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
 #endif
   }
   __syncthreads();
@@ -1121,11 +1124,11 @@ __global__ void QBA_LISTS_BOUNDS
   // the grid stride in an SGPR, read once: reloading gridDim in the loop is a
   // scalar load whose s_waitcnt lgkmcnt(0) also drains every LDS atomic the
   // wave has in flight (-2% step time)
-  const uint32_t ustride = __builtin_amdgcn_readfirstlane(gridDim.x * BS);
+  const uint32_t ustride = __builtin_amdgcn_readfirstlane(nblk * BS);
 #ifdef QBA_EXP_INTERLEAVE  // experiment builds: waves interleaved across workgroups
-  const uint32_t u0 = ((threadIdx.x >> 6) * gridDim.x + blockIdx.x) * 64 + (threadIdx.x & 63);
+  const uint32_t u0 = ((threadIdx.x >> 6) * nblk + bid) * 64 + (threadIdx.x & 63);
 #else
-  const uint32_t u0 = blockIdx.x * BS + threadIdx.x;
+  const uint32_t u0 = bid * BS + threadIdx.x;
 #endif
   if constexpr (MODE != 0 && QBA_QUEUE) {
     QbaWaveQ wq;
@@ -1159,7 +1162,7 @@ __global__ void QBA_LISTS_BOUNDS
   }
   // the remaining < 4 QPT entries: whole quads, then the partial one
   const uint32_t r0 = nunits * (4 * QPT), rq = (count - r0 + 3) >> 2;
-  if (!(QBA_EXP_SKIP & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x < rq) {
+  if (!(QBA_EXP_SKIP & 1) && bid == nblk - 1 && threadIdx.x < rq) {
     const uint32_t c0 = r0 + 4 * threadIdx.x;
     if (c0 + 4 <= count)
       qba_step_l<NP, MODE, SAMP, 1, false, PK>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
@@ -1171,7 +1174,7 @@ __global__ void QBA_LISTS_BOUNDS
 #ifdef QBA_EXP_TIMING
     const uint64_t ts2 = wall_clock64();
 #endif
-    uint4 *dst = reinterpret_cast<uint4 *>(slab + (size_t)blockIdx.x * C::NBP);
+    uint4 *dst = reinterpret_cast<uint4 *>(slab + (size_t)bid * C::NBP);
     const uint4 *src = reinterpret_cast<const uint4 *>(hist);
     if (!(QBA_EXP_SKIP & 2))
       for (int i = threadIdx.x; i < C::NBP / 4; i += BS) dst[i] = src[i];
@@ -1188,9 +1191,135 @@ __global__ void QBA_LISTS_BOUNDS
 #if QBA_ZERO_AT_END
     // any point of this kernel precedes the reduction; at the end it leaves
     // the main loop's code placement alone
-    if (blockIdx.x == gridDim.x - 1) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
+    if (bid == nblk - 1) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
 #endif
   }
+}
+
+template <int NP, int MODE, int SAMP, int QPT, int PK>
+__global__ void QBA_LISTS_BOUNDS
+    qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
+                uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
+                uint32_t *__restrict__ slab, QbaZero zero) {
+  qba_lists_body<NP, MODE, SAMP, QPT, PK>(ps, k0, k1, first, count, lists, ld, slab, zero, 0u);
+}
+
+// ---------------------------------------------------------------------------
+// Deferred slab reduction (qba_sample_check_deferred / _packed_deferred, qba.h).
+// A launch that has few list workgroups (configs[1]: 163 of 512 slots) leaves
+// CUs idle, and its separate reduce launch costs a kernel boundary per call.
+// A deferred call instead runs the PREVIOUS deferred call's reduction in W
+// extra workgroups of its own list kernel (qba_k_lists_def), on two
+// alternating slab buffers; qba_flush_deferred reduces the last one
+// (qba_k_reduce_def).  Reduce workgroup u owns everything of bin row u:
+// H[u][*][*], the pair bins C[u][*] (and, for u = 0, the stats), so it writes
+// every output word of u exactly once (plain stores, no atomics, no zeroing
+// pass): out = (acc ? out : 0) + the column sum over the slab rows, with the
+// derived words (|P_u| = sum_x H[u][0][x] -> P[u], C[u][g][g], H[u][1][u])
+// from the same sums.  Bitwise identical to qba_k_reduce's result.
+// ---------------------------------------------------------------------------
+struct QbaDefer {
+  const uint32_t *slab;  // the pending call's slab rows (NBP words apart)
+  int rows;              // its list workgroups
+  int red;               // reduce workgroups ahead of the list workgroups: W, or 0 (none pending)
+  int acc;               // the pending call accumulates into its outputs
+  int sacc;              // ... and into the stats (a later chunk of one call)
+  int64_t *H, *C, *P, *stats;
+};
+
+template <int NP>
+__host__ __device__ constexpr int qba_def_cols(int u) {  // slab columns of bin row u
+  using C = QCfg<NP>;
+  return C::G * C::WP + C::CP + (u == 0 ? C::STATS : 0);
+}
+
+// The reduce of bin row u by one workgroup of bs threads; sh: LDS scratch of
+// (bs + qba_def_cols(0)) words.
+template <int NP>
+__device__ __forceinline__ void qba_reduce_u(const QbaDefer &d, int u, int tid, int bs, uint32_t *sh) {
+  using C = QCfg<NP>;
+  typedef unsigned long long u64;
+  constexpr int NH = C::G * C::WP;
+  static_assert(qba_def_cols<NP>(0) <= QBA_LBLOCK, "one column per thread at least");
+  const int nc = qba_def_cols<NP>(u);
+  const int S = bs / nc;  // row classes: thread (col, sub) sums rows sub, sub + S, ...
+  const int col = tid % nc, sub = tid / nc;
+  if (sub < S) {
+    const int w = col < NH ? u * NH + col
+                           : col < NH + C::CP ? C::HBL + u * C::CP + (col - NH) : C::HBL + C::CBL + (col - NH - C::CP);
+    const uint32_t *src = d.slab + w;
+    uint32_t s = 0;
+    int r = sub;
+    // 8 rows in flight per thread (the rows were written by the previous
+    // kernel and come from beyond this XCD's L2)
+    for (; r + 7 * S < d.rows; r += 8 * S) {
+      uint32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = src[(size_t)(r + k * S) * C::NBP];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[k];
+    }
+    for (; r < d.rows; r += S) s += src[(size_t)r * C::NBP];
+    sh[sub * nc + col] = s;
+  }
+  __syncthreads();
+  uint32_t *tot = sh + S * nc;
+  if (tid < nc) {
+    uint32_t t = 0;
+    for (int k = 0; k < S; ++k) t += sh[k * nc + tid];
+    tot[tid] = t;  // <= the entries of one launch (< 2^32)
+  }
+  __syncthreads();
+  u64 psz = 0;  // |P_u|: group 0's bins (columns [0, W))
+#pragma unroll
+  for (int x = 0; x < C::W; ++x) psz += tot[x];
+  const bool acc = d.acc != 0;
+  for (int c = tid; c < nc; c += bs) {
+    if (c < NH) {
+      const int g = c / C::WP, x = c - g * C::WP;
+      if (x >= C::W) continue;  // row padding
+      const u64 v = g == 1 ? (x == u ? psz : 0ull) : (u64)tot[c];
+      int64_t *o = &d.H[(u * C::G + g) * C::W + x];
+      *o = (acc ? *o : 0) + (int64_t)v;
+    } else if (c < NH + C::CP) {
+      int p = c - NH, g = 0;
+      while (p >= C::G - 1 - g) p -= C::G - 1 - g++;  // pidx(g, h) inverted
+      const int h = g + 1 + p;
+      int64_t *o1 = &d.C[(u * C::G + g) * C::G + h], *o2 = &d.C[(u * C::G + h) * C::G + g];
+      *o1 = (acc ? *o1 : 0) + (int64_t)tot[c];
+      *o2 = (acc ? *o2 : 0) + (int64_t)tot[c];
+    } else if (d.stats) {
+      int64_t *o = &d.stats[c - NH - C::CP];
+      *o = (d.sacc ? *o : 0) + (int64_t)tot[c];
+    }
+  }
+  for (int g = tid; g < C::G; g += bs) {
+    int64_t *o = &d.C[(u * C::G + g) * C::G + g];
+    *o = (acc ? *o : 0) + (int64_t)psz;
+  }
+  if (tid == 0) d.P[u] = (acc ? d.P[u] : 0) + (int64_t)psz;
+}
+
+// Sample + check (MODE 1) with the pending deferred call's reduction in the
+// first d.red workgroups; the list workgroups follow (slab row = their index).
+template <int NP, int SAMP, int QPT, int PK>
+__global__ void QBA_LISTS_BOUNDS
+    qba_k_lists_def(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
+                    uint32_t count, uint8_t *__restrict__ lists, uint64_t ld, uint32_t *__restrict__ slab,
+                    QbaZero zero, QbaDefer d) {
+  extern __shared__ __align__(16) uint64_t lds[];
+  if ((int)blockIdx.x < d.red) {  // workgroup-uniform
+    qba_reduce_u<NP>(d, (int)blockIdx.x, (int)threadIdx.x, QBA_LBLOCK, reinterpret_cast<uint32_t *>(lds));
+    return;
+  }
+  qba_lists_body<NP, 1, SAMP, QPT, PK>(ps, k0, k1, first, count, lists, ld, slab, zero, (uint32_t)d.red);
+}
+
+// qba_flush_deferred: the last pending reduction on its own (grid W).
+template <int NP>
+__global__ void __launch_bounds__(QBA_LBLOCK) qba_k_reduce_def(QbaDefer d) {
+  extern __shared__ __align__(16) uint64_t lds[];
+  qba_reduce_u<NP>(d, (int)blockIdx.x, (int)threadIdx.x, QBA_LBLOCK, reinterpret_cast<uint32_t *>(lds));
 }
 
 // Batched independent instances (BASELINE configs[3]): instance i is its own
@@ -1354,7 +1483,8 @@ __global__ void __launch_bounds__(256)
 #ifndef QBA_GRID_QPT
 #define QBA_GRID_QPT 2
 #endif
-static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count, int qpt = QBA_GRID_QPT) {
+static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count, int qpt = QBA_GRID_QPT,
+                    int *cap_out = nullptr) {
   // the occupancy query costs tens of microseconds: cached per (kernel, LDS)
   struct Occ {
     const void *k;
@@ -1383,7 +1513,19 @@ static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count, 
 #endif
   if (g > cap) g = cap;
   if (g < 1) g = 1;
+  if (cap_out) *cap_out = (int)cap;
   return (int)g;
+}
+
+// qba_flush_deferred / qba_flush_pending: the pending call's reduction alone.
+template <int NP>
+static int qba_flush_def(qba_ctx *ctx) {
+  const auto &p = ctx->pend;
+  const QbaDefer d{p.slab, p.rows, 0, p.acc, p.sacc, p.H, p.C, p.P, p.stats};
+  const size_t lds = (size_t)(QBA_LBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t);
+  hipLaunchKernelGGL(qba_k_reduce_def<NP>, dim3(QCfg<NP>::W), dim3(QBA_LBLOCK), lds, p.stream, d);
+  QBA_HIP(hipGetLastError());
+  return QBA_OK;
 }
 
 // Sampler of the compiled pair: closed form when proven (n <= 11), else the
@@ -1458,19 +1600,73 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   }
 #undef QBA_K
   if (lds > 65536) QBA_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const int grid = grid_for(ctx, kern, lds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1);
-  uint32_t *slab = nullptr;
-  if (L.mode != 0) {
-    int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBP * sizeof(uint32_t));
-    if (rc) return rc;
-    slab = reinterpret_cast<uint32_t *>(ctx->slab);
-  }
+  int cap = 0;
+  const int grid = grid_for(ctx, kern, lds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1, &cap);
   const uint32_t k0 = (uint32_t)L.seed, k1 = (uint32_t)(L.seed >> 32);
   const QbaProgramSet *ps = L.ps;
   uint64_t first = L.first;
   uint32_t count = (uint32_t)L.count;
   uint8_t *lists = L.lists;
   uint64_t ld = L.ld;
+  // Deferred reduction: the list kernel also reduces the pending deferred
+  // call (W workgroups ahead of its own) when both fit the chip's resident
+  // slots together; otherwise the pending one is flushed and this call is
+  // reduced at once (its results are then simply complete earlier).
+  if (L.defer && L.mode == 1 && grid + C::W <= cap) {
+#define QBA_KD(S)                                                                                  \
+  (L.packed ? (wide ? (const void *)qba_k_lists_def<NP, S, 2, 1> : (const void *)qba_k_lists_def<NP, S, 1, 1>) \
+            : (wide ? (const void *)qba_k_lists_def<NP, S, QBA_WIDE_QPT, 0> : (const void *)qba_k_lists_def<NP, S, 1, 0>))
+    const void *kd = nullptr;
+    if (samp == QBA_S_CLOSED) {
+      if constexpr (NP <= QBA_CLOSED_MAX_N) kd = QBA_KD(QBA_S_CLOSED);
+    } else {
+      kd = samp == QBA_S_FAST ? QBA_KD(QBA_S_FAST) : QBA_KD(QBA_S_GENERAL);
+    }
+#undef QBA_KD
+    size_t dlds = lds;
+    const size_t rlds = (size_t)(QBA_LBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t);
+    if (dlds < rlds) dlds = rlds;
+    if (dlds > 65536) QBA_HIP(hipFuncSetAttribute(kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds));
+    auto &pd = ctx->pend;
+    int rc = QBA_OK;
+    // a pending call of another n or on another stream is flushed on its own
+    if (pd.flush && (pd.flush != &qba_flush_def<NP> || pd.stream != L.stream))
+      if ((rc = qba_flush_pending(ctx, L.stream))) return rc;
+    const size_t half_need = ((size_t)grid * C::NBP * sizeof(uint32_t) + 255) & ~(size_t)255;
+    if (ctx->slab_bytes < 2 * half_need) {
+      if ((rc = qba_flush_pending(ctx, L.stream))) return rc;
+      if ((rc = qba_ensure_slab(ctx, 2 * half_need))) return rc;  // synchronises before a reallocation
+    }
+    const size_t half = (ctx->slab_bytes / 2) & ~(size_t)255;
+    const int red = pd.flush ? C::W : 0;
+    const int buf = pd.flush ? pd.buf ^ 1 : 0;
+    uint32_t *slab = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(ctx->slab) + (size_t)buf * half);
+    QbaDefer d{pd.slab, pd.rows, red, pd.acc, pd.sacc, pd.H, pd.C, pd.P, pd.stats};
+    QbaZero zero{L.H, L.C, L.P, L.stats, 0u};  // the reduction writes every output word itself
+    void *args[] = {&ps, (void *)&k0, (void *)&k1, &first, &count, &lists, &ld, &slab, &zero, &d};
+    QBA_HIP(hipLaunchKernel(kd, dim3(grid + red), dim3(QBA_LBLOCK), args, dlds, L.stream));
+    QBA_HIP(hipGetLastError());
+    pd.flush = &qba_flush_def<NP>;
+    pd.slab = slab;
+    pd.rows = grid;
+    pd.acc = L.accumulate;
+    pd.sacc = L.stats_accumulate;
+    pd.buf = buf;
+    pd.H = L.H;
+    pd.C = L.C;
+    pd.P = L.P;
+    pd.stats = L.stats;
+    pd.stream = L.stream;
+    return QBA_OK;
+  }
+  if (L.mode != 0)
+    if (int rc = qba_flush_pending(ctx, L.stream)) return rc;
+  uint32_t *slab = nullptr;
+  if (L.mode != 0) {
+    int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBP * sizeof(uint32_t));
+    if (rc) return rc;
+    slab = reinterpret_cast<uint32_t *>(ctx->slab);
+  }
   QbaZero zero{L.H, L.C, L.P, L.stats,
                (L.mode != 0 && !L.accumulate ? 1u : 0u) | (L.mode != 0 && !L.stats_accumulate ? 2u : 0u)};
   void *args[] = {&ps, (void *)&k0, (void *)&k1, &first, &count, &lists, &ld, &slab, &zero};

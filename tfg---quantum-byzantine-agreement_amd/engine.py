@@ -186,16 +186,22 @@ class Engine:
 
     def sample_check(self, n: int, seed: int, first: int, count: int,
                      lists: Optional[torch.Tensor] = None, counts: Optional[Counts] = None,
-                     accumulate: bool = False) -> Tuple[torch.Tensor, Counts]:
+                     accumulate: bool = False, deferred: bool = False) -> Tuple[torch.Tensor, Counts]:
+        """deferred: qba_sample_check_deferred -- the counts are complete only
+        after the next deferred call or flush_deferred() (include/qba.h)."""
         self.prepare(n)
         if lists is None:
             lists = self.alloc_lists(n, count)
         if counts is None:
             counts = self.alloc_counts(n)
         ld = self._lists_ok(lists, n, count)
-        call("qba_sample_check", self.ctx, n, seed, first, count, _ptr(lists), ld,
-             _ptr(counts.H), _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
+        call("qba_sample_check_deferred" if deferred else "qba_sample_check", self.ctx, n, seed, first, count,
+             _ptr(lists), ld, _ptr(counts.H), _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
         return lists, counts
+
+    def flush_deferred(self) -> None:
+        """Launch the pending deferred reduction (on its call's stream)."""
+        call("qba_flush_deferred", self.ctx)
 
     def sample_packed(self, n: int, seed: int, first: int, count: int,
                       packed: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -209,17 +215,18 @@ class Engine:
 
     def sample_check_packed(self, n: int, seed: int, first: int, count: int,
                             packed: Optional[torch.Tensor] = None, counts: Optional[Counts] = None,
-                            accumulate: bool = False) -> Tuple[torch.Tensor, Counts]:
+                            accumulate: bool = False, deferred: bool = False) -> Tuple[torch.Tensor, Counts]:
         """The fused hot path writing nibble rows (half the bytes of
-        sample_check; same lists and counts)."""
+        sample_check; same lists and counts).  deferred: as sample_check."""
         self.prepare(n)
         if packed is None:
             packed = self.alloc_packed(n, count)
         if counts is None:
             counts = self.alloc_counts(n)
         ld = self._packed_ok(packed, n + 1, count)
-        call("qba_sample_check_packed", self.ctx, n, seed, first, count, _ptr(packed), ld,
-             _ptr(counts.H), _ptr(counts.C), _ptr(counts.P), int(accumulate), self.stream())
+        call("qba_sample_check_packed_deferred" if deferred else "qba_sample_check_packed", self.ctx, n, seed,
+             first, count, _ptr(packed), ld, _ptr(counts.H), _ptr(counts.C), _ptr(counts.P), int(accumulate),
+             self.stream())
         return packed, counts
 
     def sample_check_batched(self, n: int, seed_base: int, n_inst: int, count: int,
