@@ -20,7 +20,7 @@
 // qba_build_flags() reports which were compiled in (0 for a shipped build;
 // tests/test_oracle_golden.py asserts it).
 // ---------------------------------------------------------------------------
-#if defined(QBA_EXP_GTAB) || defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||            \
+#if defined(QBA_EXP_GTAB) || defined(QBA_EXP_LDSPAD) || defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||            \
     defined(QBA_EXP_NOTABLE) || defined(QBA_EXP_CHEAPRNG) || defined(QBA_EXP_PADVALU) || defined(QBA_EXP_PADLDS) || defined(QBA_EXP_DESYNC) || \
     defined(QBA_EXP_PACKSTORE) || defined(QBA_EXP_SMALLNARROW) || defined(QBA_EXP_NOATOMIC) ||          \
     defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_INTERLEAVE) ||             \

@@ -1566,6 +1566,9 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     lds += (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
     if (QBA_QUEUE) lds += (size_t)(QBA_LBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
   }
+#ifdef QBA_EXP_LDSPAD  // experiment builds: pad the launch's LDS (occupancy probe: one workgroup per CU)
+  if (L.mode == 1) lds += QBA_EXP_LDSPAD;
+#endif
   lds = (lds + 15) & ~(size_t)15;
   if (lds == 0) lds = 16;
   // 4*QPT-byte row vectors (QPT quads per thread-step) when the rows allow it
