@@ -26,7 +26,7 @@
     defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_INTERLEAVE) ||             \
     defined(QBA_EXP_GRID) || defined(QBA_EXP_NARROW) || defined(QBA_WIDE_QPT) || defined(QBA_MINW) || \
     defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) || defined(QBA_RED_ALL_IN_FLIGHT) ||           \
-    defined(QBA_QUEUE) || defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || \
+    defined(QBA_QUEUE) || defined(QBA_LATE_DRAIN) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) || defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || \
     defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N)
 #ifndef QBA_EXPERIMENT_BUILD
 #error "an experiment switch is set without QBA_EXPERIMENT_BUILD (tools/exp/build.sh): not a shippable libqba"
@@ -39,8 +39,11 @@
 #define QBA_MAX_FACTORS 16
 #define QBA_MAX_TABLE 4096   // uint64 table entries per kind (LDS budget)
 #define QBA_BLOCK 256        // threads per workgroup (batched / helper kernels)
+#ifndef QBA_SGPR_LEAN  // list kernels: round keys / row bases re-derived on the scalar unit
+#define QBA_SGPR_LEAN 1
+#endif
 #ifndef QBA_LBLOCK
-#define QBA_LBLOCK 768       // threads per workgroup of the streaming list kernels (2 per CU at n = 11)
+#define QBA_LBLOCK 1024      // threads per workgroup of the streaming list kernels (2 per CU at n = 11)
 #endif
 #define QBA_CHUNK (1ull << 31)  // entries per list-kernel launch (32-bit offsets, u32 bins)
 #define QBA_EPT 4            // entries per thread per step: one dword per list row
@@ -58,8 +61,11 @@ __device__ __forceinline__ uint32_t qba_xor3(uint32_t a, uint32_t b, uint32_t k)
 }
 
 // Keys are wave-uniform (kernel arguments or block-uniform): they stay in SGPRs.
-__device__ __forceinline__ QbaU4 qba_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                            uint32_t k0, uint32_t k1) {
+// SK (QBA_SGPR_LEAN callers with wave-uniform keys): round keys re-derived per
+// block on the scalar unit.
+template <bool SK = false>
+__device__ __forceinline__ QbaU4 qba_philox_k(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1) {
 #ifdef QBA_EXP_CHEAPRNG  // experiment builds only (tools/exp): cost of the generator
   const uint32_t h = (c0 ^ k0) * 0x9E3779B9u + c1 + c2 * 0x85EBCA6Bu;
   return QbaU4{h, h * 0xC2B2AE35u, h ^ (h >> 15) ^ k1, (h * 0x27D4EB2Fu) ^ c3};
@@ -76,8 +82,15 @@ __device__ __forceinline__ QbaU4 qba_philox(uint32_t c0, uint32_t c1, uint32_t c
     c2 = n2;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
+    // the round keys re-derived per block on the scalar unit (two s_add per
+    // round) instead of 20 loop-invariant SGPRs (register budget of 8 waves)
+    if constexpr (SK) asm volatile("" : "+s"(k0), "+s"(k1));
   }
   return QbaU4{c0, c1, c2, c3};
+}
+__device__ __forceinline__ QbaU4 qba_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1) {
+  return qba_philox_k<false>(c0, c1, c2, c3, k0, k1);
 }
 
 // ---------------------------------------------------------------------------

@@ -30,6 +30,12 @@
 #ifndef QBA_QTAB_MASK  // stage-table reads by the Q-correlated lanes only (experiment)
 #define QBA_QTAB_MASK 0
 #endif
+#ifndef QBA_PAIRWISE  // closed sampler: a quad's two pairs one after the other (fewer live VGPRs)
+#define QBA_PAIRWISE 1
+#endif
+#ifndef QBA_LATE_DRAIN  // fused kernel: a full queue batch is read at once, counted after the next quad's table reads
+#define QBA_LATE_DRAIN 0
+#endif
 #ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
 #define QBA_NT_STORE 1
 #endif
@@ -570,14 +576,41 @@ __device__ __forceinline__ void qba_entry_d(uint64_t e, uint32_t k0, uint32_t k1
 }
 
 // Sample one quad (entries [c0, c0+4) of the launch) into the byte layout.
-template <int NP, int SAMP, bool TAIL>
+struct QbaNoHook {
+  __device__ void operator()() const {}
+};
+// hook(): called once the quad's stage-table reads are issued (QBA_LATE_DRAIN)
+template <int NP, int SAMP, bool TAIL, typename Hook = QbaNoHook>
 __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t first, uint32_t k0,
                                                 uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                                 const uint64_t *pat, const uint64_t *apat,
                                                 const uint64_t *thr, const uint32_t *pl,
-                                                uint32_t (&D)[4][CF<NP>::ND]) {
+                                                uint32_t (&D)[4][CF<NP>::ND], const Hook &hook = Hook()) {
   constexpr int ND = CF<NP>::ND;
   if constexpr (SAMP == QBA_S_CLOSED && !TAIL) {
+#if QBA_PAIRWISE  // each pair's table reads and finish before the next pair's Philox (fewer live VGPRs)
+    if (!(first & 1)) {
+      const uint32_t phi = (uint32_t)(first >> 33);
+      const uint32_t plo = (uint32_t)(first >> 1) + (c0 >> 1);
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        QbaClosed cl[2];
+        const uint64_t p = ((uint64_t)phi << 32) | (uint64_t)(plo + (uint32_t)jp);
+        const QbaU4 x = qba_philox_k<QBA_SGPR_LEAN != 0>(plo + (uint32_t)jp, phi, 0u, 0u, k0, k1);
+        qba_closed_rank<NP>(x.x, x.y, p, 0u, k0, k1, cl[0]);
+        qba_closed_rank<NP>(x.z, x.w, p, 1u, k0, k1, cl[1]);
+        uint4 A[2];
+        uint2 sB[2];
+        uint32_t sC[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) qba_closed_tables<NP>(cl[j].rank, pl, A[j], sB[j], sC[j]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) qba_closed_finish<NP>(cl[j], A[j], sB[j], sC[j], D[2 * jp + j]);
+      }
+      hook();
+      return;
+    }
+#endif
     if (!(first & 1)) {  // wave-uniform: the quad is two whole pairs
       QbaClosed cl[4];
       // A launch never crosses a multiple of 2^33 entries (dispatch splits
@@ -611,6 +644,7 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
 #pragma unroll
       for (int j = 0; j < 4; ++j) qba_closed_tables<NP>(cl[j].rank, pl, A[j], sB[j], sC[j]);
 #endif
+      hook();
 #pragma unroll
       for (int j = 0; j < 4; ++j) qba_closed_finish<NP>(cl[j], A[j], sB[j], sC[j], D[j]);
       return;
@@ -625,6 +659,7 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
       for (int i = 0; i < ND; ++i) D[j][i] = 0;
     }
   }
+  hook();
 }
 
 // Every value of a quad of entries < W?  One OR over the quad's transposed
@@ -673,6 +708,8 @@ struct QbaWaveQ {
   uint32_t base;      // LDS byte address of this wave's ring [ND][QBA_QCAP] words (aligned to 4 QBA_QCAP B)
   uint32_t tail, qn;  // wave-uniform: first queued slot (not reduced mod QBA_QCAP), queued entries
   uint32_t hoff;      // LDS byte address of the histogram, kept in a VGPR (see qba_count_d)
+  uint32_t pd[4];     // QBA_LATE_DRAIN: a batch of 64 entries read from the ring, not yet counted
+  uint32_t pn;        // wave-uniform: pd holds a batch (0 / 1)
 };
 
 // LDS byte address of ring slot s (any integer: taken mod QBA_QCAP); the
@@ -708,6 +745,35 @@ __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_
   q.qn -= nv;
 }
 
+// QBA_LATE_DRAIN: count the batch held in registers (if any).  Called by the
+// fused step after a quad's stage-table reads are issued, so that those reads
+// do not queue behind this batch's atomics and the batch's ring reads (issued
+// a quad earlier) have long completed.
+template <int NP>
+__device__ __forceinline__ void qba_q_count_held(QbaWaveQ &q, uint32_t *hist) {
+  constexpr int ND = CF<NP>::ND;
+  if (q.pn) {
+    uint32_t D[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) D[i] = q.pd[i];
+    qba_count_d<NP>(D, 0x00010001u, hist, true, true, q.hoff);
+    q.pn = 0;
+  }
+}
+// Read the 64 oldest queued entries into registers (their slots are free at
+// once: LDS executes a wave's reads before its later writes).
+template <int NP>
+__device__ __forceinline__ void qba_q_hold(QbaWaveQ &q, uint32_t *hist) {
+  constexpr int ND = CF<NP>::ND;
+  qba_q_count_held<NP>(q, hist);  // a second batch before the count point: count the first now
+  const uint32_t a = qba_q_addr(q, q.tail + __lane_id());
+#pragma unroll
+  for (int i = 0; i < ND; ++i) q.pd[i] = *qba_lds(a + i * QBA_QCAP * 4);
+  q.pn = 1;
+  q.tail += 64;
+  q.qn -= 64;
+}
+
 // Append the lanes' entries with isq set (in lane order) and count a full
 // batch of 64 as soon as one is queued.  Slot = tail + qn + the number of
 // queued lanes below this one (mbcnt adds the base for free).
@@ -725,7 +791,12 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
     for (int i = 0; i < ND; ++i) *qba_lds(a + i * QBA_QCAP * 4) = D[i];
   }
   q.qn += (uint32_t)__popcll(m);
-  if (q.qn >= 64) qba_q_drain<NP, TRUSTED>(q, hist, 64u);
+  if (q.qn >= 64) {
+    if (QBA_LATE_DRAIN && TRUSTED)
+      qba_q_hold<NP>(q, hist);
+    else
+      qba_q_drain<NP, TRUSTED>(q, hist, 64u);
+  }
 }
 
 // One thread-step over QPT consecutive quads: entries [c0, c0 + 4 QPT) of the
@@ -733,7 +804,7 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
 // 4*QPT-byte vector per thread (16 B at QPT = 4: a wave moves 1 KiB per row).
 // MODE 0: sample -> lists;  MODE 1: sample -> lists + counts;  MODE 2: lists -> counts
 // TAIL (QPT = 1 only): the last, partial quad, byte by byte.
-template <int NP, int MODE, int SAMP, int QPT, bool TAIL>
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false>
 __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                          uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                          const uint64_t *pat, const uint64_t *apat,
@@ -774,7 +845,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
       for (int i = 0; i < ND; ++i)
         qba_t4(row[k][4 * i], row[k][4 * i + 1], row[k][4 * i + 2], row[k][4 * i + 3], D[0][i],
                D[1][i], D[2][i], D[3][i]);
-      if (wq) {
+      if constexpr (WQ) {  // the caller's queue (never null)
 #pragma unroll
         for (int j = 0; j < 4; ++j) qba_q_push<NP, MODE == 1>(*wq, D[j], qba_isq_d<NP>(D[j], am), hist);
       } else {
@@ -790,7 +861,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
         qba_t4(D[0][i], D[1][i], D[2][i], D[3][i], row[k][4 * i], row[k][4 * i + 1],
                row[k][4 * i + 2], row[k][4 * i + 3]);
       if constexpr (MODE == 1) {
-        if (wq) {
+        if constexpr (WQ) {  // the caller's queue (never null)
           // L0 != L1 (tfg.py:327) of the quad's 4 entries at once: byte j of
           // row 0 XOR row 1 is nonzero iff entry j is Q-correlated
           const uint32_t xq = (row[k][0] ^ row[k][1]) & (act ? 0xffffffffu : 0u);
@@ -882,7 +953,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
 // QPT = 1 (unaligned starts, the tail quads): 2 bytes per row, stored as bytes
 // (a chunk may start at an odd byte).  MODE 2 reads the same layout; an
 // unpacked quad's entries come out permuted (counting is order-free).
-template <int NP, int MODE, int SAMP, int QPT, bool TAIL>
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false>
 __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                             uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                             const uint64_t *pat, const uint64_t *apat,
@@ -931,7 +1002,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
       for (int i = 0; i < ND; ++i)
         qba_t4(row[k][4 * i], row[k][4 * i + 1], row[k][4 * i + 2], row[k][4 * i + 3], D[0][i],
                D[1][i], D[2][i], D[3][i]);
-      if (wq) {
+      if constexpr (WQ) {  // the caller's queue (never null)
 #pragma unroll
         for (int j = 0; j < 4; ++j) qba_q_push<NP, false>(*wq, D[j], qba_isq_d<NP>(D[j], am), hist);
       } else {
@@ -943,14 +1014,18 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
     const uint32_t am = act ? 0xffu : 0u;
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
-      qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
+      if constexpr (MODE == 1 && QBA_LATE_DRAIN && WQ)  // WQ: wq is the caller's queue (never null)
+        qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D,
+                                        [&] { qba_q_count_held<NP>(*wq, hist); });
+      else
+        qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
         Dp[2 * k][i] = D[0][i] | (D[1][i] << 4);
         Dp[2 * k + 1][i] = D[2][i] | (D[3][i] << 4);
       }
       if constexpr (MODE == 1) {
-        if (wq) {
+        if constexpr (WQ) {  // the caller's queue (never null)
           // L0 != L1 (tfg.py:327) of a pair at once: nibble 0 / 1 of
           // (byte 0 ^ byte 1) of its packed word 0 is entry 2p / 2p+1's test
 #pragma unroll
@@ -968,6 +1043,8 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
       }
     }
     if (!TAIL && act) {
+      uint64_t rbl = 0;  // QBA_SGPR_LEAN: the running row base
+      (void)rbl;
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
         uint32_t r[4];
@@ -980,8 +1057,21 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
           const int g = 4 * i + gg;
           if (g >= C::G) continue;
           // row base opaque in SGPRs, 32-bit lane offset (as qba_step)
+#if QBA_SGPR_LEAN
+          // one running row pointer (s_add_u32 / s_addc_u32 per row) instead
+          // of n+1 loop-invariant 64-bit bases
+          if (g == 0) {
+            rbl = reinterpret_cast<uint64_t>(lists);
+            asm volatile("" : "+s"(rbl));
+          } else {
+            rbl += ld;
+            asm volatile("" : "+s"(rbl));
+          }
+          const uint64_t rb = rbl;
+#else
           uint64_t rb = reinterpret_cast<uint64_t>(lists) + (uint64_t)g * ld;
           asm("" : "+s"(rb));
+#endif
           if constexpr (QPT == 2) {
 #if QBA_NT_STORE
             __builtin_nontemporal_store(r[gg], reinterpret_cast<GU *>(rb + cb));
@@ -1008,7 +1098,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
   }
 }
 
-template <int NP, int MODE, int SAMP, int QPT, bool TAIL, int PK>
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, int PK, bool WQ = false>
 __device__ __forceinline__ void qba_step_l(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                            uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                            const uint64_t *pat, const uint64_t *apat,
@@ -1016,9 +1106,9 @@ __device__ __forceinline__ void qba_step_l(uint32_t c0, uint32_t count, uint64_t
                                            uint8_t *__restrict__ lists, uint64_t ld, uint32_t *hist,
                                            QbaWaveQ *wq = nullptr, bool act = true) {
   if constexpr (PK)
-    qba_step_pk<NP, MODE, SAMP, QPT, TAIL>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
+    qba_step_pk<NP, MODE, SAMP, QPT, TAIL, WQ>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
   else
-    qba_step<NP, MODE, SAMP, QPT, TAIL>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
+    qba_step<NP, MODE, SAMP, QPT, TAIL, WQ>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
 }
 
 // Stage the program's tables in LDS; returns the histogram base after them.
@@ -1083,10 +1173,19 @@ __device__ __forceinline__ void qba_zero_outputs(const QbaZero &z, int tid, int 
   if ((z.flags & 2) && z.stats && tid < C::STATS) z.stats[tid] = 0;
 }
 
+// Waves per SIMD the list kernels are compiled for.  The closed-form sampler
+// runs 2 workgroups of 1024 threads per CU = 8 waves per SIMD (the CDNA4
+// maximum): with its quads sampled pair by pair (QBA_PAIRWISE) and the round
+// keys / row bases re-derived on the scalar unit (QBA_SGPR_LEAN) it fits the
+// 64 VGPRs and the SGPR budget that needs, and the extra waves hide the LDS
+// latency of the histogram atomics: -3 % cycles per launch against 6 waves
+// of 768 threads (profiles/r3/r3k).  The table samplers (n > 11) need more
+// registers and keep the compiler's choice.
 #ifdef QBA_MINW  // experiment builds: minimum waves per SIMD (caps the VGPRs)
 #define QBA_LISTS_BOUNDS __launch_bounds__(QBA_LBLOCK, QBA_MINW)
 #else
-#define QBA_LISTS_BOUNDS __launch_bounds__(QBA_LBLOCK)
+#define QBA_LISTS_BOUNDS \
+  __attribute__((amdgpu_flat_work_group_size(1, QBA_LBLOCK), amdgpu_waves_per_eu(SAMP == QBA_S_CLOSED ? 8 : 1)))
 #endif
 // PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row.
 // The body of the list kernel; its workgroups are those after the first
@@ -1135,6 +1234,7 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
     wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
     wq.qn = 0;
+    wq.pn = 0;
     wq.hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     asm("" : "+v"(wq.hoff));  // held in a VGPR (no instruction is emitted)
 #ifdef QBA_EXP_DESYNC  // experiment builds: stagger the waves' phase at the start (s_sleep units of 64 cycles)
@@ -1151,9 +1251,10 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
     for (uint32_t u = u0;; u += ustride) {
       const bool act = u < nunits;
       if (!__any(act)) break;
-      qba_step_l<NP, MODE, SAMP, QPT, false, PK>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
-                                           lists, ld, hist, &wq, act);
+      qba_step_l<NP, MODE, SAMP, QPT, false, PK, true>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
+                                                 lists, ld, hist, &wq, act);
     }
+    qba_q_count_held<NP>(wq, hist);
     while (wq.qn) qba_q_drain<NP, MODE == 1>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
   } else {
     for (uint32_t u = u0; u < nunits; u += ustride)
@@ -1350,14 +1451,16 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
     wq.qn = 0;
+    wq.pn = 0;
     wq.hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     asm("" : "+v"(wq.hoff));
     for (uint32_t u = threadIdx.x;; u += QBA_BLOCK) {  // wave-uniform trip count
       const bool act = u < nunits;
       if (!__any(act)) break;
-      qba_step_l<NP, 1, SAMP, QPT, false, PK>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,
-                                        hist, &wq, act);
+      qba_step_l<NP, 1, SAMP, QPT, false, PK, true>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl,
+                                              L, ld, hist, &wq, act);
     }
+    qba_q_count_held<NP>(wq, hist);
     while (wq.qn) qba_q_drain<NP, true>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
 #else
     for (uint32_t u = threadIdx.x; u < nunits; u += QBA_BLOCK)

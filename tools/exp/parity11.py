@@ -13,7 +13,8 @@ sys.path.insert(0, root)
 sys.path.insert(0, os.path.join(root, "oracle"))
 import oracle_lib  # noqa: E402
 
-eng = importlib.import_module("tfg---quantum-byzantine-agreement_amd.engine").Engine(0)
+eng_mod = importlib.import_module("tfg---quantum-byzantine-agreement_amd.engine")
+eng = eng_mod.Engine(0)
 n = 11
 info = eng.prepare(n)
 ok = True
@@ -28,6 +29,12 @@ for first, count in [(0, 1), (0, 4099), (1, 5001), (6, 100_003), (1 << 33, 262_1
         good = np.array_equal(got, ref) and np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
         s = eng.sample(n, 4242, first, count)[:, :count].cpu().numpy()
         good = good and np.array_equal(s, ref)
+        # the nibble-row hot path (qba_sample_check_packed)
+        pk, c2 = eng.sample_check_packed(n, 4242, first, count)
+        torch.cuda.synchronize()
+        gH, gC, gP = c2.numpy()
+        good = good and np.array_equal(eng_mod.unpack_nibbles(pk.cpu().numpy(), count), ref)
+        good = good and np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
         ok = ok and good
     print(f"first={first} count={count}: {'ok' if good else 'MISMATCH'}")
 print("PARITY", "OK" if ok else "FAILED")

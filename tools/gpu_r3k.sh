@@ -1,7 +1,12 @@
 #!/bin/bash
-# Occupancy probe for LDS-hungry counting layouts: the shipped kernel vs the
-# same kernel forced to one workgroup per CU (768 and 1024 threads).
+# Occupancy (896 threads at 7 waves/SIMD, 640 threads), late-drain (with and
+# without a 6-wave register cap) and compile-time queue variants of the fused
+# kernel vs the shipped one; parity of every variant first.
 set -eo pipefail
 root=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $root
-ROUNDS=2 bash tools/exp/ab.sh r3k/ab2
+mkdir -p gpurun_out/r3k
+for so in o_lean1024m8 q_lean768; do
+  QBA_LIB=$root/tfg---quantum-byzantine-agreement_amd/_build/exp/$so.so timeout -k 10 200 python -u tools/exp/parity11.py > gpurun_out/r3k/parity_$so.txt 2>&1
+done
+ROUNDS=2 bash tools/exp/ab.sh r3k/ab4
