@@ -437,9 +437,15 @@ __device__ __forceinline__ void qba_t4(uint32_t a, uint32_t b, uint32_t c, uint3
 // v_pk_lshlrev_b16: each 16-bit half of `one` shifted by the low 4 bits of
 // the same half of `amt` (the upper bits of the half are ignored by the ALU).
 __device__ __forceinline__ uint32_t qba_pk_onehot(uint32_t amt, uint32_t one) {
+#if QBA_PK_BUILTIN  // experiment builds: the compiler's v_pk_lshlrev_b16 (no asm hazard padding)
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  const us2 a = __builtin_bit_cast(us2, amt & 0x000f000fu), o = __builtin_bit_cast(us2, one);
+  return __builtin_bit_cast(uint32_t, (us2)(o << a));
+#else
   uint32_t r;
   asm("v_pk_lshlrev_b16 %0, %1, %2" : "=v"(r) : "v"(amt), "v"(one));
   return r;
+#endif
 }
 
 typedef __attribute__((address_space(3))) uint32_t qba_lds_u32;  // LDS word (32-bit address)
@@ -1078,6 +1084,9 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
 #else
             *reinterpret_cast<GU *>(rb + cb) = r[gg];
 #endif
+          } else if (!((reinterpret_cast<uintptr_t>(lists) | ld) & 1)) {  // uniform: rows 2-byte aligned (cb is even)
+            typedef __attribute__((address_space(1))) uint16_t GH;
+            *reinterpret_cast<GH *>(rb + cb) = (uint16_t)r[gg];
           } else {
             uint8_t *d = reinterpret_cast<uint8_t *>(rb + cb);
             d[0] = (uint8_t)r[gg];
@@ -1333,53 +1342,72 @@ __host__ __device__ constexpr int qba_def_cols(int u) {  // slab columns of bin 
   using C = QCfg<NP>;
   return C::G * C::WP + C::CP + (u == 0 ? C::STATS : 0);
 }
-
-// The reduce of bin row u by one workgroup of bs threads; sh: LDS scratch of
-// (bs + qba_def_cols(0)) words.
+// Workgroups per bin row: part 0 owns columns [0, 2 WP) at least (groups 0
+// and 1: |P_u| and every word derived from it), the other parts split the rest.
 template <int NP>
-__device__ __forceinline__ void qba_reduce_u(const QbaDefer &d, int u, int tid, int bs, uint32_t *sh) {
+__host__ __device__ constexpr int qba_def_parts() {
+  using C = QCfg<NP>;
+  return qba_def_cols<NP>(1) >= 8 * C::WP ? 4 : 1;
+}
+template <int NP>
+__host__ __device__ constexpr int qba_def_wgs() {  // reduce workgroups of one deferred reduction
+  return QCfg<NP>::W * qba_def_parts<NP>();
+}
+
+// The reduce of part `part` of bin row u by one workgroup of bs threads; sh:
+// LDS scratch of (bs + qba_def_cols(0)) words.
+template <int NP>
+__device__ __forceinline__ void qba_reduce_u(const QbaDefer &d, int u, int part, int tid, int bs, uint32_t *sh) {
   using C = QCfg<NP>;
   typedef unsigned long long u64;
-  constexpr int NH = C::G * C::WP;
+  constexpr int NH = C::G * C::WP, NP4 = qba_def_parts<NP>();
   static_assert(qba_def_cols<NP>(0) <= QBA_LBLOCK, "one column per thread at least");
-  const int nc = qba_def_cols<NP>(u);
+  const int ncu = qba_def_cols<NP>(u);
+  constexpr int SPAN = (qba_def_cols<NP>(1) + NP4 - 1) / NP4;
+  constexpr int SPAN0 = NP4 == 1 ? qba_def_cols<NP>(0) : (SPAN > 2 * C::WP ? SPAN : 2 * C::WP);
+  constexpr int REST = NP4 == 1 ? 1 : (qba_def_cols<NP>(1) - SPAN0 + NP4 - 2) / (NP4 - 1);
+  const int c0 = part == 0 ? 0 : SPAN0 + (part - 1) * REST;
+  const int c1 = part == 0 ? (SPAN0 < ncu ? SPAN0 : ncu) : (part == NP4 - 1 ? ncu : c0 + REST);
+  const int nc = c1 - c0;
   const int S = bs / nc;  // row classes: thread (col, sub) sums rows sub, sub + S, ...
-  const int col = tid % nc, sub = tid / nc;
+  const int col = c0 + tid % nc, sub = tid / nc;
   if (sub < S) {
     const int w = col < NH ? u * NH + col
                            : col < NH + C::CP ? C::HBL + u * C::CP + (col - NH) : C::HBL + C::CBL + (col - NH - C::CP);
     const uint32_t *src = d.slab + w;
     uint32_t s = 0;
     int r = sub;
-    // 8 rows in flight per thread (the rows were written by the previous
+    // 16 rows in flight per thread (the rows were written by the previous
     // kernel and come from beyond this XCD's L2)
-    for (; r + 7 * S < d.rows; r += 8 * S) {
-      uint32_t v[8];
+    for (; r + 15 * S < d.rows; r += 16 * S) {
+      uint32_t v[16];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = src[(size_t)(r + k * S) * C::NBP];
+      for (int k = 0; k < 16; ++k) v[k] = src[(size_t)(r + k * S) * C::NBP];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s += v[k];
+      for (int k = 0; k < 16; ++k) s += v[k];
     }
     for (; r < d.rows; r += S) s += src[(size_t)r * C::NBP];
-    sh[sub * nc + col] = s;
+    sh[sub * nc + (col - c0)] = s;
   }
   __syncthreads();
-  uint32_t *tot = sh + S * nc;
+  uint32_t *tot = sh + S * nc;  // tot[c - c0]
   if (tid < nc) {
     uint32_t t = 0;
     for (int k = 0; k < S; ++k) t += sh[k * nc + tid];
     tot[tid] = t;  // <= the entries of one launch (< 2^32)
   }
   __syncthreads();
-  u64 psz = 0;  // |P_u|: group 0's bins (columns [0, W))
+  u64 psz = 0;  // |P_u|: group 0's bins (columns [0, W), part 0)
+  if (part == 0) {
 #pragma unroll
-  for (int x = 0; x < C::W; ++x) psz += tot[x];
+    for (int x = 0; x < C::W; ++x) psz += tot[x];
+  }
   const bool acc = d.acc != 0;
-  for (int c = tid; c < nc; c += bs) {
+  for (int c = c0 + tid; c < c1; c += bs) {
     if (c < NH) {
       const int g = c / C::WP, x = c - g * C::WP;
       if (x >= C::W) continue;  // row padding
-      const u64 v = g == 1 ? (x == u ? psz : 0ull) : (u64)tot[c];
+      const u64 v = g == 1 ? (x == u ? psz : 0ull) : (u64)tot[c - c0];  // group 1: part 0 (c < 2 WP)
       int64_t *o = &d.H[(u * C::G + g) * C::W + x];
       *o = (acc ? *o : 0) + (int64_t)v;
     } else if (c < NH + C::CP) {
@@ -1387,18 +1415,20 @@ __device__ __forceinline__ void qba_reduce_u(const QbaDefer &d, int u, int tid, 
       while (p >= C::G - 1 - g) p -= C::G - 1 - g++;  // pidx(g, h) inverted
       const int h = g + 1 + p;
       int64_t *o1 = &d.C[(u * C::G + g) * C::G + h], *o2 = &d.C[(u * C::G + h) * C::G + g];
-      *o1 = (acc ? *o1 : 0) + (int64_t)tot[c];
-      *o2 = (acc ? *o2 : 0) + (int64_t)tot[c];
+      *o1 = (acc ? *o1 : 0) + (int64_t)tot[c - c0];
+      *o2 = (acc ? *o2 : 0) + (int64_t)tot[c - c0];
     } else if (d.stats) {
       int64_t *o = &d.stats[c - NH - C::CP];
-      *o = (d.sacc ? *o : 0) + (int64_t)tot[c];
+      *o = (d.sacc ? *o : 0) + (int64_t)tot[c - c0];
     }
   }
-  for (int g = tid; g < C::G; g += bs) {
-    int64_t *o = &d.C[(u * C::G + g) * C::G + g];
-    *o = (acc ? *o : 0) + (int64_t)psz;
+  if (part == 0) {
+    for (int g = tid; g < C::G; g += bs) {
+      int64_t *o = &d.C[(u * C::G + g) * C::G + g];
+      *o = (acc ? *o : 0) + (int64_t)psz;
+    }
+    if (tid == 0) d.P[u] = (acc ? d.P[u] : 0) + (int64_t)psz;
   }
-  if (tid == 0) d.P[u] = (acc ? d.P[u] : 0) + (int64_t)psz;
 }
 
 // Sample + check (MODE 1) with the pending deferred call's reduction in the
@@ -1410,17 +1440,21 @@ __global__ void QBA_LISTS_BOUNDS
                     QbaZero zero, QbaDefer d) {
   extern __shared__ __align__(16) uint64_t lds[];
   if ((int)blockIdx.x < d.red) {  // workgroup-uniform
-    qba_reduce_u<NP>(d, (int)blockIdx.x, (int)threadIdx.x, QBA_LBLOCK, reinterpret_cast<uint32_t *>(lds));
+    constexpr int NP4 = qba_def_parts<NP>();
+    qba_reduce_u<NP>(d, (int)blockIdx.x / NP4, (int)blockIdx.x % NP4, (int)threadIdx.x, QBA_LBLOCK,
+                     reinterpret_cast<uint32_t *>(lds));
     return;
   }
   qba_lists_body<NP, 1, SAMP, QPT, PK>(ps, k0, k1, first, count, lists, ld, slab, zero, (uint32_t)d.red);
 }
 
-// qba_flush_deferred: the last pending reduction on its own (grid W).
+// qba_flush_deferred: the last pending reduction on its own.
 template <int NP>
 __global__ void __launch_bounds__(QBA_LBLOCK) qba_k_reduce_def(QbaDefer d) {
   extern __shared__ __align__(16) uint64_t lds[];
-  qba_reduce_u<NP>(d, (int)blockIdx.x, (int)threadIdx.x, QBA_LBLOCK, reinterpret_cast<uint32_t *>(lds));
+  constexpr int NP4 = qba_def_parts<NP>();
+  qba_reduce_u<NP>(d, (int)blockIdx.x / NP4, (int)blockIdx.x % NP4, (int)threadIdx.x, QBA_LBLOCK,
+                   reinterpret_cast<uint32_t *>(lds));
 }
 
 // Batched independent instances (BASELINE configs[3]): instance i is its own
@@ -1626,7 +1660,7 @@ static int qba_flush_def(qba_ctx *ctx) {
   const auto &p = ctx->pend;
   const QbaDefer d{p.slab, p.rows, 0, p.acc, p.sacc, p.H, p.C, p.P, p.stats};
   const size_t lds = (size_t)(QBA_LBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t);
-  hipLaunchKernelGGL(qba_k_reduce_def<NP>, dim3(QCfg<NP>::W), dim3(QBA_LBLOCK), lds, p.stream, d);
+  hipLaunchKernelGGL(qba_k_reduce_def<NP>, dim3(qba_def_wgs<NP>()), dim3(QBA_LBLOCK), lds, p.stream, d);
   QBA_HIP(hipGetLastError());
   return QBA_OK;
 }
@@ -1682,6 +1716,10 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
 #ifdef QBA_EXP_SMALLNARROW  // experiment builds: launches below this many entries take the narrow kernel on a wider grid
   const bool small = L.count < (uint64_t)QBA_EXP_SMALLNARROW;
 #else
+  // (the one-quad step on twice the workgroups shortens a small launch's list
+  // kernel -- 8.8 vs 10.1 us at 1e6 entries -- but its workgroups then share
+  // CUs with the deferred reduction's: 11.7 vs 10.3 us per configs[1] step,
+  // profiles/r3/r3m, r3n; not taken)
   const bool small = false;
 #endif
   // nibble rows: the wide step stores one 4-B word per row (QPT = 2)
@@ -1718,7 +1756,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   // call (W workgroups ahead of its own) when both fit the chip's resident
   // slots together; otherwise the pending one is flushed and this call is
   // reduced at once (its results are then simply complete earlier).
-  if (L.defer && L.mode == 1 && grid + C::W <= cap) {
+  if (L.defer && L.mode == 1 && grid + qba_def_wgs<NP>() <= cap) {
 #define QBA_KD(S)                                                                                  \
   (L.packed ? (wide ? (const void *)qba_k_lists_def<NP, S, 2, 1> : (const void *)qba_k_lists_def<NP, S, 1, 1>) \
             : (wide ? (const void *)qba_k_lists_def<NP, S, QBA_WIDE_QPT, 0> : (const void *)qba_k_lists_def<NP, S, 1, 0>))
@@ -1744,7 +1782,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
       if ((rc = qba_ensure_slab(ctx, 2 * half_need))) return rc;  // synchronises before a reallocation
     }
     const size_t half = (ctx->slab_bytes / 2) & ~(size_t)255;
-    const int red = pd.flush ? C::W : 0;
+    const int red = pd.flush ? qba_def_wgs<NP>() : 0;
     const int buf = pd.flush ? pd.buf ^ 1 : 0;
     uint32_t *slab = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(ctx->slab) + (size_t)buf * half);
     QbaDefer d{pd.slab, pd.rows, red, pd.acc, pd.sacc, pd.H, pd.C, pd.P, pd.stats};
