@@ -26,7 +26,7 @@
     defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_INTERLEAVE) ||             \
     defined(QBA_EXP_GRID) || defined(QBA_EXP_NARROW) || defined(QBA_WIDE_QPT) || defined(QBA_MINW) || \
     defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) || defined(QBA_RED_ALL_IN_FLIGHT) ||           \
-    defined(QBA_QUEUE) || defined(QBA_LATE_DRAIN) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) || defined(QBA_PK_BUILTIN) || defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || \
+    defined(QBA_QUEUE) || defined(QBA_LATE_DRAIN) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) || defined(QBA_PK_BUILTIN) || defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) || \
     defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N)
 #ifndef QBA_EXPERIMENT_BUILD
 #error "an experiment switch is set without QBA_EXPERIMENT_BUILD (tools/exp/build.sh): not a shippable libqba"
@@ -44,6 +44,9 @@
 #endif
 #ifndef QBA_LBLOCK
 #define QBA_LBLOCK 1024      // threads per workgroup of the streaming list kernels (2 per CU at n = 11)
+#endif
+#ifndef QBA_DBLOCK
+#define QBA_DBLOCK 768       // ... of the deferred-reduction list kernel (small launches)
 #endif
 #define QBA_CHUNK (1ull << 31)  // entries per list-kernel launch (32-bit offsets, u32 bins)
 #define QBA_EPT 4            // entries per thread per step: one dword per list row

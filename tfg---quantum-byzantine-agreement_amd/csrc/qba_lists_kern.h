@@ -1199,13 +1199,12 @@ __device__ __forceinline__ void qba_zero_outputs(const QbaZero &z, int tid, int 
 // PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row.
 // The body of the list kernel; its workgroups are those after the first
 // `red` (qba_k_lists: 0; qba_k_lists_def: its reduce workgroups).
-template <int NP, int MODE, int SAMP, int QPT, int PK>
+template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK>
 __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1,
                                                uint64_t first, uint32_t count, uint8_t *__restrict__ lists,
                                                uint64_t ld, uint32_t *__restrict__ slab, QbaZero zero,
                                                uint32_t red) {
   using C = QCfg<NP>;
-  constexpr int BS = QBA_LBLOCK;
   extern __shared__ __align__(16) uint64_t lds[];
   const uint32_t bid = blockIdx.x - red, nblk = gridDim.x - red;
   const uint64_t *pat, *apat, *thr;
@@ -1361,7 +1360,7 @@ __device__ __forceinline__ void qba_reduce_u(const QbaDefer &d, int u, int part,
   using C = QCfg<NP>;
   typedef unsigned long long u64;
   constexpr int NH = C::G * C::WP, NP4 = qba_def_parts<NP>();
-  static_assert(qba_def_cols<NP>(0) <= QBA_LBLOCK, "one column per thread at least");
+  static_assert(qba_def_cols<NP>(0) <= QBA_DBLOCK && QBA_DBLOCK <= QBA_LBLOCK, "one column per thread at least");
   const int ncu = qba_def_cols<NP>(u);
   constexpr int SPAN = (qba_def_cols<NP>(1) + NP4 - 1) / NP4;
   constexpr int SPAN0 = NP4 == 1 ? qba_def_cols<NP>(0) : (SPAN > 2 * C::WP ? SPAN : 2 * C::WP);
@@ -1434,18 +1433,20 @@ __device__ __forceinline__ void qba_reduce_u(const QbaDefer &d, int u, int part,
 // Sample + check (MODE 1) with the pending deferred call's reduction in the
 // first d.red workgroups; the list workgroups follow (slab row = their index).
 template <int NP, int SAMP, int QPT, int PK>
-__global__ void QBA_LISTS_BOUNDS
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, QBA_DBLOCK),
+                               amdgpu_waves_per_eu(SAMP == QBA_S_CLOSED ? 6 : 1)))
     qba_k_lists_def(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                     uint32_t count, uint8_t *__restrict__ lists, uint64_t ld, uint32_t *__restrict__ slab,
                     QbaZero zero, QbaDefer d) {
   extern __shared__ __align__(16) uint64_t lds[];
   if ((int)blockIdx.x < d.red) {  // workgroup-uniform
     constexpr int NP4 = qba_def_parts<NP>();
-    qba_reduce_u<NP>(d, (int)blockIdx.x / NP4, (int)blockIdx.x % NP4, (int)threadIdx.x, QBA_LBLOCK,
+    qba_reduce_u<NP>(d, (int)blockIdx.x / NP4, (int)blockIdx.x % NP4, (int)threadIdx.x, QBA_DBLOCK,
                      reinterpret_cast<uint32_t *>(lds));
     return;
   }
-  qba_lists_body<NP, 1, SAMP, QPT, PK>(ps, k0, k1, first, count, lists, ld, slab, zero, (uint32_t)d.red);
+  qba_lists_body<NP, 1, SAMP, QPT, PK, QBA_DBLOCK>(ps, k0, k1, first, count, lists, ld, slab, zero,
+                                                   (uint32_t)d.red);
 }
 
 // qba_flush_deferred: the last pending reduction on its own.
@@ -1621,7 +1622,7 @@ __global__ void __launch_bounds__(256)
 #define QBA_GRID_QPT 2
 #endif
 static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count, int qpt = QBA_GRID_QPT,
-                    int *cap_out = nullptr) {
+                    int *cap_out = nullptr, int bs = QBA_LBLOCK) {
   // the occupancy query costs tens of microseconds: cached per (kernel, LDS)
   struct Occ {
     const void *k;
@@ -1634,7 +1635,7 @@ static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count, 
   for (const Occ &o : cache)
     if (o.k == kern && o.lds == lds) per_cu = o.per_cu;
   if (per_cu == 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, QBA_LBLOCK, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, bs, lds) != hipSuccess ||
         per_cu < 1)
       per_cu = 1;
     cache[next] = Occ{kern, lds, per_cu};
@@ -1643,7 +1644,7 @@ static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count, 
   const uint64_t nquad = (count + 3) >> 2;
   // >= 2 quads (one wide thread-step) per thread: a small launch (configs[1],
   // 1e6 entries) spreads over 163 workgroups instead of 82
-  uint64_t g = (nquad + qpt * QBA_LBLOCK - 1) / (qpt * QBA_LBLOCK);
+  uint64_t g = (nquad + (uint64_t)qpt * bs - 1) / ((uint64_t)qpt * bs);
   const uint64_t cap = (uint64_t)ctx->num_cus * (uint64_t)per_cu;
 #ifdef QBA_EXP_GRID  // experiment builds: grid from the environment (QBA_EXP_GRID=<workgroups>)
   if (const char *e = getenv("QBA_EXP_GRID")) g = strtoull(e, nullptr, 10);
@@ -1756,21 +1757,33 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   // call (W workgroups ahead of its own) when both fit the chip's resident
   // slots together; otherwise the pending one is flushed and this call is
   // reduced at once (its results are then simply complete earlier).
-  if (L.defer && L.mode == 1 && grid + qba_def_wgs<NP>() <= cap) {
+  const void *kd = nullptr;
+  if (L.defer && L.mode == 1) {
 #define QBA_KD(S)                                                                                  \
   (L.packed ? (wide ? (const void *)qba_k_lists_def<NP, S, 2, 1> : (const void *)qba_k_lists_def<NP, S, 1, 1>) \
             : (wide ? (const void *)qba_k_lists_def<NP, S, QBA_WIDE_QPT, 0> : (const void *)qba_k_lists_def<NP, S, 1, 0>))
-    const void *kd = nullptr;
     if (samp == QBA_S_CLOSED) {
       if constexpr (NP <= QBA_CLOSED_MAX_N) kd = QBA_KD(QBA_S_CLOSED);
     } else {
       kd = samp == QBA_S_FAST ? QBA_KD(QBA_S_FAST) : QBA_KD(QBA_S_GENERAL);
     }
 #undef QBA_KD
-    size_t dlds = lds;
-    const size_t rlds = (size_t)(QBA_LBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t);
+  }
+  // the deferred kernel runs QBA_DBLOCK-thread workgroups (small launches:
+  // more, shorter workgroups; 9.6 vs 10.5 us per configs[1] pass)
+  size_t dlds = 0;
+  int dgrid = 0, dcap = 0;
+  if (kd) {
+    dlds = table_lds<NP>(hs, samp) + (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
+    if (QBA_QUEUE) dlds += (size_t)(QBA_DBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
+    const size_t rlds = (size_t)(QBA_DBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t);
     if (dlds < rlds) dlds = rlds;
+    dlds = (dlds + 15) & ~(size_t)15;
     if (dlds > 65536) QBA_HIP(hipFuncSetAttribute(kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds));
+    dgrid = grid_for(ctx, kd, dlds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1, &dcap, QBA_DBLOCK);
+  }
+  if (kd && dgrid + qba_def_wgs<NP>() <= dcap) {
+    const int grid = dgrid;
     auto &pd = ctx->pend;
     int rc = QBA_OK;
     // a pending call of another n or on another stream is flushed on its own
@@ -1788,7 +1801,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     QbaDefer d{pd.slab, pd.rows, red, pd.acc, pd.sacc, pd.H, pd.C, pd.P, pd.stats};
     QbaZero zero{L.H, L.C, L.P, L.stats, 0u};  // the reduction writes every output word itself
     void *args[] = {&ps, (void *)&k0, (void *)&k1, &first, &count, &lists, &ld, &slab, &zero, &d};
-    QBA_HIP(hipLaunchKernel(kd, dim3(grid + red), dim3(QBA_LBLOCK), args, dlds, L.stream));
+    QBA_HIP(hipLaunchKernel(kd, dim3(grid + red), dim3(QBA_DBLOCK), args, dlds, L.stream));
     QBA_HIP(hipGetLastError());
     pd.flush = &qba_flush_def<NP>;
     pd.slab = slab;
