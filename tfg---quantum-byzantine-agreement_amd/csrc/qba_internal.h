@@ -26,7 +26,7 @@
     defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_INTERLEAVE) ||             \
     defined(QBA_EXP_GRID) || defined(QBA_EXP_NARROW) || defined(QBA_WIDE_QPT) || defined(QBA_MINW) || \
     defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) || defined(QBA_RED_ALL_IN_FLIGHT) ||           \
-    defined(QBA_QUEUE) || defined(QBA_LATE_DRAIN) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) || defined(QBA_PK_BUILTIN) || defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) || \
+    defined(QBA_QUEUE) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) || defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) || \
     defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N)
 #ifndef QBA_EXPERIMENT_BUILD
 #error "an experiment switch is set without QBA_EXPERIMENT_BUILD (tools/exp/build.sh): not a shippable libqba"

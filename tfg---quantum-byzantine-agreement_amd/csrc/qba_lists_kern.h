@@ -33,9 +33,6 @@
 #ifndef QBA_PAIRWISE  // closed sampler: a quad's two pairs one after the other (fewer live VGPRs)
 #define QBA_PAIRWISE 1
 #endif
-#ifndef QBA_LATE_DRAIN  // fused kernel: a full queue batch is read at once, counted after the next quad's table reads
-#define QBA_LATE_DRAIN 0
-#endif
 #ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
 #define QBA_NT_STORE 1
 #endif
@@ -437,15 +434,9 @@ __device__ __forceinline__ void qba_t4(uint32_t a, uint32_t b, uint32_t c, uint3
 // v_pk_lshlrev_b16: each 16-bit half of `one` shifted by the low 4 bits of
 // the same half of `amt` (the upper bits of the half are ignored by the ALU).
 __device__ __forceinline__ uint32_t qba_pk_onehot(uint32_t amt, uint32_t one) {
-#if QBA_PK_BUILTIN  // experiment builds: the compiler's v_pk_lshlrev_b16 (no asm hazard padding)
-  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-  const us2 a = __builtin_bit_cast(us2, amt & 0x000f000fu), o = __builtin_bit_cast(us2, one);
-  return __builtin_bit_cast(uint32_t, (us2)(o << a));
-#else
   uint32_t r;
   asm("v_pk_lshlrev_b16 %0, %1, %2" : "=v"(r) : "v"(amt), "v"(one));
   return r;
-#endif
 }
 
 typedef __attribute__((address_space(3))) uint32_t qba_lds_u32;  // LDS word (32-bit address)
@@ -582,16 +573,12 @@ __device__ __forceinline__ void qba_entry_d(uint64_t e, uint32_t k0, uint32_t k1
 }
 
 // Sample one quad (entries [c0, c0+4) of the launch) into the byte layout.
-struct QbaNoHook {
-  __device__ void operator()() const {}
-};
-// hook(): called once the quad's stage-table reads are issued (QBA_LATE_DRAIN)
-template <int NP, int SAMP, bool TAIL, typename Hook = QbaNoHook>
+template <int NP, int SAMP, bool TAIL>
 __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t first, uint32_t k0,
                                                 uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                                 const uint64_t *pat, const uint64_t *apat,
                                                 const uint64_t *thr, const uint32_t *pl,
-                                                uint32_t (&D)[4][CF<NP>::ND], const Hook &hook = Hook()) {
+                                                uint32_t (&D)[4][CF<NP>::ND]) {
   constexpr int ND = CF<NP>::ND;
   if constexpr (SAMP == QBA_S_CLOSED && !TAIL) {
 #if QBA_PAIRWISE  // each pair's table reads and finish before the next pair's Philox (fewer live VGPRs)
@@ -613,7 +600,6 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
 #pragma unroll
         for (int j = 0; j < 2; ++j) qba_closed_finish<NP>(cl[j], A[j], sB[j], sC[j], D[2 * jp + j]);
       }
-      hook();
       return;
     }
 #endif
@@ -650,7 +636,6 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
 #pragma unroll
       for (int j = 0; j < 4; ++j) qba_closed_tables<NP>(cl[j].rank, pl, A[j], sB[j], sC[j]);
 #endif
-      hook();
 #pragma unroll
       for (int j = 0; j < 4; ++j) qba_closed_finish<NP>(cl[j], A[j], sB[j], sC[j], D[j]);
       return;
@@ -665,7 +650,6 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
       for (int i = 0; i < ND; ++i) D[j][i] = 0;
     }
   }
-  hook();
 }
 
 // Every value of a quad of entries < W?  One OR over the quad's transposed
@@ -714,8 +698,6 @@ struct QbaWaveQ {
   uint32_t base;      // LDS byte address of this wave's ring [ND][QBA_QCAP] words (aligned to 4 QBA_QCAP B)
   uint32_t tail, qn;  // wave-uniform: first queued slot (not reduced mod QBA_QCAP), queued entries
   uint32_t hoff;      // LDS byte address of the histogram, kept in a VGPR (see qba_count_d)
-  uint32_t pd[4];     // QBA_LATE_DRAIN: a batch of 64 entries read from the ring, not yet counted
-  uint32_t pn;        // wave-uniform: pd holds a batch (0 / 1)
 };
 
 // LDS byte address of ring slot s (any integer: taken mod QBA_QCAP); the
@@ -751,35 +733,6 @@ __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_
   q.qn -= nv;
 }
 
-// QBA_LATE_DRAIN: count the batch held in registers (if any).  Called by the
-// fused step after a quad's stage-table reads are issued, so that those reads
-// do not queue behind this batch's atomics and the batch's ring reads (issued
-// a quad earlier) have long completed.
-template <int NP>
-__device__ __forceinline__ void qba_q_count_held(QbaWaveQ &q, uint32_t *hist) {
-  constexpr int ND = CF<NP>::ND;
-  if (q.pn) {
-    uint32_t D[ND];
-#pragma unroll
-    for (int i = 0; i < ND; ++i) D[i] = q.pd[i];
-    qba_count_d<NP>(D, 0x00010001u, hist, true, true, q.hoff);
-    q.pn = 0;
-  }
-}
-// Read the 64 oldest queued entries into registers (their slots are free at
-// once: LDS executes a wave's reads before its later writes).
-template <int NP>
-__device__ __forceinline__ void qba_q_hold(QbaWaveQ &q, uint32_t *hist) {
-  constexpr int ND = CF<NP>::ND;
-  qba_q_count_held<NP>(q, hist);  // a second batch before the count point: count the first now
-  const uint32_t a = qba_q_addr(q, q.tail + __lane_id());
-#pragma unroll
-  for (int i = 0; i < ND; ++i) q.pd[i] = *qba_lds(a + i * QBA_QCAP * 4);
-  q.pn = 1;
-  q.tail += 64;
-  q.qn -= 64;
-}
-
 // Append the lanes' entries with isq set (in lane order) and count a full
 // batch of 64 as soon as one is queued.  Slot = tail + qn + the number of
 // queued lanes below this one (mbcnt adds the base for free).
@@ -797,12 +750,7 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
     for (int i = 0; i < ND; ++i) *qba_lds(a + i * QBA_QCAP * 4) = D[i];
   }
   q.qn += (uint32_t)__popcll(m);
-  if (q.qn >= 64) {
-    if (QBA_LATE_DRAIN && TRUSTED)
-      qba_q_hold<NP>(q, hist);
-    else
-      qba_q_drain<NP, TRUSTED>(q, hist, 64u);
-  }
+  if (q.qn >= 64) qba_q_drain<NP, TRUSTED>(q, hist, 64u);
 }
 
 // One thread-step over QPT consecutive quads: entries [c0, c0 + 4 QPT) of the
@@ -1020,11 +968,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
     const uint32_t am = act ? 0xffu : 0u;
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
-      if constexpr (MODE == 1 && QBA_LATE_DRAIN && WQ)  // WQ: wq is the caller's queue (never null)
-        qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D,
-                                        [&] { qba_q_count_held<NP>(*wq, hist); });
-      else
-        qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
+      qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
         Dp[2 * k][i] = D[0][i] | (D[1][i] << 4);
@@ -1242,7 +1186,6 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
     wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
     wq.qn = 0;
-    wq.pn = 0;
     wq.hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     asm("" : "+v"(wq.hoff));  // held in a VGPR (no instruction is emitted)
 #ifdef QBA_EXP_DESYNC  // experiment builds: stagger the waves' phase at the start (s_sleep units of 64 cycles)
@@ -1262,7 +1205,6 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
       qba_step_l<NP, MODE, SAMP, QPT, false, PK, true>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
                                                  lists, ld, hist, &wq, act);
     }
-    qba_q_count_held<NP>(wq, hist);
     while (wq.qn) qba_q_drain<NP, MODE == 1>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
   } else {
     for (uint32_t u = u0; u < nunits; u += ustride)
@@ -1486,7 +1428,6 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
     wq.qn = 0;
-    wq.pn = 0;
     wq.hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     asm("" : "+v"(wq.hoff));
     for (uint32_t u = threadIdx.x;; u += QBA_BLOCK) {  // wave-uniform trip count
@@ -1495,7 +1436,6 @@ __global__ void __launch_bounds__(QBA_BLOCK)
       qba_step_l<NP, 1, SAMP, QPT, false, PK, true>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl,
                                               L, ld, hist, &wq, act);
     }
-    qba_q_count_held<NP>(wq, hist);
     while (wq.qn) qba_q_drain<NP, true>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
 #else
     for (uint32_t u = threadIdx.x; u < nunits; u += QBA_BLOCK)
