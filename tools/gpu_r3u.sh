@@ -4,7 +4,7 @@
 # list-kernel time over launches 5-299 of a 300-launch trace, two passes.
 set -eo pipefail
 root=${GRAFT_REPO_ROOT:-$(pwd)}
-out=$root/gpurun_out/r3u; mkdir -p $out
+out=$root/gpurun_out/r3u2; mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 for r in 1 2; do
   for so in $root/tfg---quantum-byzantine-agreement_amd/_build/exp/*.so; do
