@@ -143,6 +143,69 @@ def _lib_sha16():
     return hashlib.sha256(Path(lib.LIB_PATH).read_bytes()).hexdigest()[:16]
 
 
+GOLDEN_TOTALS = ROOT / "tests" / "golden" / "config2_totals_n11_5eed.npz"
+
+
+def golden_counts(n, seed, per, world):
+    """The C twin's H, C, P over entries [0, per * world) when that is a
+    prefix tests/golden/gen_config2_totals.py recorded (n = 11, seed 0x5EED,
+    1.25e8 entries per rank, world 1, 2, 4 or 8 -- world 8 is sizeL = 1e9),
+    else None.  A fixture (data), not the oracle: the weak-scaling line checks
+    its own all-reduced counts with it."""
+    if n != 11 or seed != 0x5EED or per != 125_000_000 or world not in (1, 2, 4, 8) or not GOLDEN_TOTALS.exists():
+        return None
+    import numpy as np
+    z = np.load(GOLDEN_TOTALS)
+    return z[f"H_{world}"], z[f"C_{world}"], z[f"P_{world}"]
+
+
+def verify_counts(n, seed, per, world, H, C, P):
+    """bench.py's verification block for one set of all-reduced counts."""
+    import numpy as np
+    offdiag = int(C.sum() - sum(C[:, g, g].sum() for g in range(n + 1)))
+    out = {"q_entries": int(P.sum()), "offdiag_collisions": offdiag}
+    ref = golden_counts(n, seed, per, world)
+    if ref is not None:
+        same = bool(np.array_equal(H, ref[0]) and np.array_equal(C, ref[1]) and np.array_equal(P, ref[2]))
+        out["counts_equal_golden"] = same
+        out["golden"] = (f"C-twin H/C/P over entries [0, {per * world}) "
+                         f"(tests/golden/{GOLDEN_TOTALS.name}, key {world})")
+        if per * world == 10 ** 9:
+            out["counts_equal_1e9_golden"] = same
+    return out
+
+
+def issue_roofline(tj, entries, launch_ms):
+    """roofline.issue: the fused kernel's issue-side ceiling from the PMC
+    counters of this build (tools/pmc_traffic.py: chip-wide medians per
+    launch).  Shader cycles per launch = GRBM_GUI_ACTIVE / 8 (8 XCDs); a
+    wave64 VALU instruction issues in 2 cycles on a 32-lane CDNA4 SIMD, 1,024
+    SIMDs and 256 LDS units on the chip."""
+    c = tj.get("issue_counters_per_launch") or {}
+    if "GRBM_GUI_ACTIVE" not in c or "SQ_INSTS_VALU" not in c:
+        return None
+    cyc = c["GRBM_GUI_ACTIVE"] / 8
+    valu_ipc = c["SQ_INSTS_VALU"] / (1024 * cyc)
+    out = {"cycles_per_launch": cyc,
+           "effective_clock_ghz": cyc / (launch_ms * 1e6) if launch_ms else None,
+           "valu_lane_ops_per_entry": c["SQ_INSTS_VALU"] * 64 / entries,
+           "valu_insts_per_simd_cycle": valu_ipc,
+           "valu_busy_frac": 2 * valu_ipc}
+    if "SQ_LDS_IDX_ACTIVE" in c:
+        out["lds_active_frac"] = c["SQ_LDS_IDX_ACTIVE"] / (256 * cyc)
+        out["lds_bank_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(c["SQ_LDS_IDX_ACTIVE"], 1.0)
+    if "SQ_INSTS_LDS_ATOMIC" in c:
+        out["lds_atomics_per_entry"] = c["SQ_INSTS_LDS_ATOMIC"] * 64 / entries
+    if "SQ_INSTS_LDS" in c:
+        out["lds_insts_per_entry"] = c["SQ_INSTS_LDS"] * 64 / entries
+    busy = {"VALU": out["valu_busy_frac"], "LDS": out.get("lds_active_frac", 0.0)}
+    top = max(busy, key=busy.get)
+    out["binds"] = (f"{top} issue ({busy[top]:.0%} busy; "
+                    + ", ".join(f"{k} {v:.0%}" for k, v in busy.items() if k != top)
+                    + "): neither unit saturated, the rest is LDS / memory latency the 8 waves per SIMD do not hide")
+    return out
+
+
 # ---------------------------------------------------------------------------
 # configs[2]: the headline (default)
 # ---------------------------------------------------------------------------
@@ -235,10 +298,18 @@ def headline(args):
     else:
         kern_ms = ev[0][0].elapsed_time(ev[0][1]) / args.steps
     H, C, P = counts[(args.steps - 1) % nbuf].H, counts[(args.steps - 1) % nbuf].C, counts[(args.steps - 1) % nbuf].P
+    # every rank's own launch time (HIP events on its stream), for diagnosing a flat scaling curve
+    kt = torch.tensor([kern_ms], dtype=torch.float64, device=eng.device)
+    if world > 1:
+        ks = [torch.zeros_like(kt) for _ in range(world)]
+        torch.distributed.all_gather(ks, kt)
+        rank_ms = [float(k.item()) for k in ks]
+    else:
+        rank_ms = [kern_ms]
 
-    # verification result of the last step: honest Q positions never collide
+    # verification result of the last step (the all-reduced counts): honest Q
+    # positions never collide, and against the C twin's totals when recorded
     Hn, Cn, Pn = (x.cpu().numpy() for x in (H, C, P))
-    offdiag = int(Cn.sum() - sum(Cn[:, g, g].sum() for g in range(n + 1)))
     if rank != 0:
         eng.close()
         return
@@ -246,7 +317,7 @@ def headline(args):
     value = entries / t_max
     bytes_per_entry = 2 * (n + 1)
     achieved = bytes_per_entry * per / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_note = None, "no PMC traffic file for this workload"
+    traffic, traffic_note, issue = None, "no PMC traffic file for this workload", None
     tp = Path(args.traffic)
     if tp.exists():
         tj = json.loads(tp.read_text())
@@ -255,6 +326,9 @@ def headline(args):
                 tj.get("layout", "bytes") == args.layout:
             if tj.get("libqba_sha16") == sha:
                 traffic, traffic_note = tj.get("hbm_bytes_per_launch"), f"PMC FETCH+WRITE of this build ({sha})"
+                issue = issue_roofline(tj, per, kern_ms)
+                if issue is not None:
+                    issue["source"] = f"PMC passes of this build ({sha}), tools/pmc_traffic.py"
             else:
                 traffic_note = f"stale: {tp.name} was measured on build {tj.get('libqba_sha16')}, running {sha}"
     out = {
@@ -268,7 +342,7 @@ def headline(args):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8",
+        "dtype": "u4 lists (nibble rows), i64 counts" if packed else "u8 lists (byte rows), i64 counts",
         "data": DATA,
         "config": {
             "workload": f"BASELINE configs[2] shard: n={n} parties, {args.dishonest} dishonest, "
@@ -294,12 +368,14 @@ def headline(args):
             "traffic_gbs": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
             "traffic_frac": traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
             "traffic_source": traffic_note,
+            "issue": issue,
             "note": "achieved/frac count the BASELINE's 24 B/entry (byte lists written + read back once); the "
                     "fused kernel writes them once and never re-reads"
                     + (", as nibble rows (6 B/entry at n=11)" if packed else "")
                     + ", so the bytes HBM really moves are traffic (traffic_gbs / traffic_frac)",
         },
-        "verification": {"q_entries": int(Pn.sum()), "offdiag_collisions": offdiag},
+        "verification": verify_counts(n, args.seed, per, world, Hn, Cn, Pn),
+        "rank_launch_ms": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_counts(n, args.seed, info, args.cpu_seconds)

@@ -144,7 +144,9 @@ QBA_API int qba_check_counts(qba_ctx *ctx, int n_parties, const uint8_t *lists_d
                      int accumulate, qba_stream stream);
 /* Statistics of the last counts launch on this ctx (synchronous):
  * out[0] = Q-correlated entries that held a value >= w and were therefore
- * not counted (never happens for lists from qba_sample), out[1] reserved. */
+ * not counted (never happens for lists from qba_sample); out[1] = workgroups
+ * of the fused n = 11 kernel whose 8-bit pair bins wrapped and that recounted
+ * their entries exactly from the stored rows (0 unless forced: QBA_LIST_GRID). */
 QBA_API int qba_last_stats(qba_ctx *ctx, int64_t *out2_host);
 /* Fused sample + check: lists are written once and counted from registers. */
 QBA_API int qba_sample_check(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,

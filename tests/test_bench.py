@@ -51,13 +51,56 @@ def test_bench_self_launch_two_ranks_gpu():
     honest lists verified collision-free."""
     env = _env(QBA_SHARE_DEVICE="1", QBA_DIST_BACKEND="gloo", QBA_BENCH_LAUNCH_TIMEOUT="150")
     p = subprocess.run([sys.executable, "-u", str(ROOT / "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2",
-                        "--per-gpu", "2.5e7"], env=env, capture_output=True, text=True, timeout=180)
+                        "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=180)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout
     line = lines[0]
     assert line["n_gpus"] == 2 and line["steps"] == 5 and line["warmup"] == 2
-    assert line["config"]["sizeL"] == 2 * 25_000_000 and line["value"] > 0
-    assert line["verification"]["offdiag_collisions"] == 0
-    # the reduced P counts both shards' Q entries: about half of 2 x 2.5e7
-    assert abs(line["verification"]["q_entries"] - 25_000_000) < 50_000
+    assert line["config"]["sizeL"] == 2 * 125_000_000 and line["value"] > 0
+    v = line["verification"]
+    assert v["offdiag_collisions"] == 0
+    # the reduced counts are the C twin's over entries [0, 2.5e8) (the recorded
+    # prefix of configs[2]); at 8 ranks the same check is counts_equal_1e9_golden
+    assert v["counts_equal_golden"] is True, v
+    assert "counts_equal_1e9_golden" not in v
+    rl = line["rank_launch_ms"]
+    assert len(rl["per_rank"]) == 2 and 0 < rl["min"] <= rl["max"]
+
+
+def test_bench_golden_verification_cpu():
+    """bench.verify_counts on the recorded configs[2] prefixes: equal counts
+    pass, one changed count fails, sizes without a fixture report none, and
+    world 8 (sizeL = 1e9) names the 1e9 check explicitly."""
+    import importlib.util
+    import numpy as np
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    for world in (1, 2, 4, 8):
+        H, C, P = (x.copy() for x in b.golden_counts(11, 0x5EED, 125_000_000, world))
+        assert int(C.sum()) == int(P.sum()) * 12  # honest: every Q entry collision-free
+        v = b.verify_counts(11, 0x5EED, 125_000_000, world, H, C, P)
+        assert v["counts_equal_golden"] is True and v["offdiag_collisions"] == 0
+        assert ("counts_equal_1e9_golden" in v) == (world == 8)
+        H[3, 4, 5] += 1
+        assert b.verify_counts(11, 0x5EED, 125_000_000, world, H, C, P)["counts_equal_golden"] is False
+    assert b.golden_counts(11, 0x5EED, 1e6, 1) is None and b.golden_counts(11, 1, 125_000_000, 1) is None
+    assert "counts_equal_golden" not in b.verify_counts(11, 7, 125_000_000, 2, H, C, P)
+    # shard 0 is what BENCH_r03's single-GPU line reported as q_entries
+    assert int(b.golden_counts(11, 0x5EED, 125_000_000, 1)[2].sum()) == 62_495_452
+    assert int(b.golden_counts(11, 0x5EED, 125_000_000, 8)[2].sum()) == 500_010_356  # |P| over sizeL = 1e9
+
+
+def test_config2_totals_fixture_matches_c_twin_shard0():
+    """The fixture's first prefix (entries [0, 1.25e8)) recomputed by the C
+    twin's closed-form schedule (a few seconds on the host)."""
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_lib
+    z = np.load(ROOT / "tests" / "golden" / "config2_totals_n11_5eed.npz")
+    empty = {"nfac": 0, "desc": np.zeros((16, 6), np.int32), "pat": np.zeros(1, np.uint64),
+             "apat": np.zeros(1, np.uint64), "thr": np.zeros(1, np.uint64)}
+    H, C, P, bad = oracle_lib.stream_counts(11, 0x5EED, 0, 125_000_000, empty, empty, closed=True)
+    assert bad == 0
+    assert np.array_equal(H, z["H_1"]) and np.array_equal(C, z["C_1"]) and np.array_equal(P, z["P_1"])

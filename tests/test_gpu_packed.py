@@ -193,3 +193,45 @@ def test_packed_batched_instances(engine, n, count):
         assert np.array_equal(c.H[i].cpu().numpy(), H)
         assert np.array_equal(c.C[i].cpu().numpy(), C)
         assert np.array_equal(c.P[i].cpu().numpy(), P)
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_pairbin_wrap_recount_exact(monkeypatch, packed):
+    """The fused n = 11 kernel counts in 8-bit pair bins (qba_lists_kern.h,
+    QbaPB).  QBA_LIST_GRID = 2 puts ~2e6 entries on each of two workgroups, so
+    every pair bin wraps many times; the flush's lane-total test must see it
+    and the workgroups recount their rows exactly (stats[1] = 2).  Lists and
+    counts stay bit-exact against the C twin, for both row layouts."""
+    monkeypatch.setenv("QBA_LIST_GRID", "2")
+    eng = sub("engine").Engine(0)
+    try:
+        n, seed, first, count = 11, 0xBADC0DE, 6, 4_000_003
+        ref = _ref(eng, n, seed, first, count)
+        if packed:
+            p, c = eng.sample_check_packed(n, seed, first, count)
+            got = _unpack(p, count)
+        else:
+            lists, c = eng.sample_check(n, seed, first, count)
+            torch.cuda.synchronize()
+            got = lists[:, :count].cpu().numpy()
+        assert np.array_equal(got, ref)
+        assert _same_counts(c, ref)
+        st = eng.last_stats()
+        assert st[0] == 0 and st[1] == 2, st
+    finally:
+        eng.close()
+
+
+def test_pairbin_no_recount_at_bench_size(engine):
+    """At the headline launch (1.25e8 entries, <= 2^18 per workgroup) no pair
+    bin wraps: no workgroup recounts (stats[1] == 0), and the counts of the
+    packed fused pass equal the check-only kernel's (32-bit bins) on its rows."""
+    n, seed, count = 11, 0x5EED, 125_000_000
+    p, c = engine.sample_check_packed(n, seed, 0, count)
+    st = engine.last_stats()
+    assert st[0] == 0 and st[1] == 0, st
+    c2 = engine.check_counts_packed(p, n, count)
+    for a, b in zip(c.numpy(), c2.numpy()):
+        assert np.array_equal(a, b)
+    del p
+    torch.cuda.empty_cache()

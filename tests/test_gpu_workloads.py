@@ -55,28 +55,49 @@ def _assert_counts(c, H, C, P, what):
     assert np.array_equal(gP, P), f"{what}: P differs"
 
 
-def test_config2_sizeL_1e9_all_shards(engine):
+_C2_TOTALS = {}
+
+
+def _config2_totals(info, n, seed, sizeL):
+    """The C twin's streaming counts over all 1e9 entries (computed once)."""
+    key = (n, seed, sizeL)
+    if key not in _C2_TOTALS:
+        _C2_TOTALS[key] = oracle_lib.stream_counts(n, seed, 0, sizeL, info["notq"], info["q"], info["closed"])
+    return _C2_TOTALS[key]
+
+
+@pytest.mark.parametrize("layout", ["packed", "bytes"])
+def test_config2_sizeL_1e9_all_shards(engine, layout):
     """BASELINE configs[2]: n = 11, sizeL = 1e9 as 8 shards of 1.25e8 entries
     (the per-GPU workload of the 8-GPU run); counts summed over the shards
-    (what the RCCL all-reduce produces) == the C twin over all 1e9 entries."""
+    (what the RCCL all-reduce produces) == the C twin over all 1e9 entries.
+    "packed" runs exactly the kernel and layout bench.py times
+    (qba_sample_check_packed: nibble rows, pair-bin counting); "bytes" the
+    byte-row form of the same fused kernel."""
     dist = sub("distributed")
     n, sizeL, world, seed = 11, 10 ** 9, 8, 0x5EED
     info = engine.prepare(n)
     per = dist.shard_bounds(sizeL, 0, world)[1]
-    lists = engine.alloc_lists(n, per)
+    packed = layout == "packed"
+    lists = engine.alloc_packed(n, per) if packed else engine.alloc_lists(n, per)
     total = engine.alloc_counts(n)
     for r in range(world):
         first, count = dist.shard_bounds(sizeL, r, world)
-        engine.sample_check(n, seed, first, count, lists, total, accumulate=r > 0)
+        if packed:
+            engine.sample_check_packed(n, seed, first, count, lists, total, accumulate=r > 0)
+        else:
+            engine.sample_check(n, seed, first, count, lists, total, accumulate=r > 0)
     torch.cuda.synchronize()
-    # lists of the last shard, three windows, byte for byte
+    # lists of the last shard, three windows, value for value
     first, count = dist.shard_bounds(sizeL, world - 1, world)
     for a, b in _windows(count):
         ref = oracle_lib.sample(n, seed, first + a, b - a, info["notq"], info["q"], info["closed"])
-        assert np.array_equal(lists[:, a:b].cpu().numpy(), ref), (a, b)
-    H, C, P, bad = oracle_lib.stream_counts(n, seed, 0, sizeL, info["notq"], info["q"], info["closed"])
+        got = (sub("engine").unpack_nibbles(lists[:, a // 2:(b + 1) // 2].cpu().numpy(), b - a) if packed
+               else lists[:, a:b].cpu().numpy())
+        assert np.array_equal(got, ref), (a, b)
+    H, C, P, bad = _config2_totals(info, n, seed, sizeL)
     assert bad == 0
-    _assert_counts(total, H, C, P, "sizeL=1e9")
+    _assert_counts(total, H, C, P, f"sizeL=1e9 ({layout})")
     # honest lists: every Q position collision-free, |P| ~ sizeL / 2
     assert C.sum() == P.sum() * (n + 1)
     assert abs(P.sum() - sizeL / 2) < 6 * math.sqrt(sizeL / 4)
@@ -146,18 +167,23 @@ def test_phi_span_crossing_unaligned_first(engine, col):
     _assert_counts(c, H, C, P, f"2^33 crossing, column {col}")
 
 
-def test_config3_full_batched(engine):
+@pytest.mark.parametrize("layout", ["bytes", "packed"])
+def test_config3_full_batched(engine, layout):
     """BASELINE configs[3]: 4096 independent 7-party instances x sizeL = 1e5
-    per GPU; every instance's counts vs the C twin, 16 instances' lists."""
+    per GPU; every instance's counts vs the C twin, 16 instances' lists.
+    "packed" is the nibble-row form bench.py --config 3 times."""
     n, n_inst, count, base = 7, 4096, 100_000, 0x5EED
     info = engine.prepare(n)
-    lists, c = engine.sample_check_batched(n, base, n_inst, count)
+    packed = layout == "packed"
+    lists, c = engine.sample_check_batched(n, base, n_inst, count, packed=packed)
     torch.cuda.synchronize()
     H, C, P = oracle_lib.batched_counts(n, base, n_inst, count, info["notq"], info["q"], info["closed"])
-    _assert_counts(c, H, C, P, "batched")
+    _assert_counts(c, H, C, P, f"batched ({layout})")
     for i in np.linspace(0, n_inst - 1, 16).astype(int):
         ref = oracle_lib.sample(n, base + int(i), 0, count, info["notq"], info["q"], info["closed"])
-        assert np.array_equal(lists[i, :, :count].cpu().numpy(), ref), i
+        got = (sub("engine").unpack_nibbles(lists[i].cpu().numpy(), count) if packed
+               else lists[i, :, :count].cpu().numpy())
+        assert np.array_equal(got, ref), i
     del lists, c
     torch.cuda.empty_cache()
 

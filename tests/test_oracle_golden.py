@@ -176,7 +176,7 @@ def test_shipped_library_has_no_experiment_switch():
     assert lib.qba_build_flags() == 0
     csrc = ROOT / "tfg---quantum-byzantine-agreement_amd" / "csrc"
     r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "--offload-arch=gfx950", "-fsyntax-only",
-                        "-DQBA_EXP_NOTABLE", "-x", "hip", str(csrc / "qba_ctx.hip")],
+                        "-DQBA_PAIRBINS=0", "-x", "hip", str(csrc / "qba_ctx.hip")],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "QBA_EXPERIMENT_BUILD" in r.stderr
 

@@ -47,6 +47,10 @@ extern "C" int qba_init(int device, qba_ctx **out) {
     const unsigned long long v = strtoull(c, nullptr, 10) & ~3ull;
     if (v >= 4 && v <= QBA_CHUNK) ctx->chunk = v;
   }
+  if (const char *c = getenv("QBA_LIST_GRID")) {  // tests: force many entries per workgroup
+    const long v = strtol(c, nullptr, 10);
+    if (v > 0 && v < (1l << 20)) ctx->list_grid = (int)v;
+  }
   if (hipMalloc(&ctx->flag, 64) != hipSuccess || hipMalloc(&ctx->count1, 64) != hipSuccess ||
       hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess) {
     qba_destroy(ctx);

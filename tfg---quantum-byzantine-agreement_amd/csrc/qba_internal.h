@@ -20,14 +20,13 @@
 // qba_build_flags() reports which were compiled in (0 for a shipped build;
 // tests/test_oracle_golden.py asserts it).
 // ---------------------------------------------------------------------------
-#if defined(QBA_EXP_GTAB) || defined(QBA_EXP_LDSPAD) || defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||            \
-    defined(QBA_EXP_NOTABLE) || defined(QBA_EXP_CHEAPRNG) || defined(QBA_EXP_PADVALU) || defined(QBA_EXP_PADLDS) || defined(QBA_EXP_DESYNC) || \
-    defined(QBA_EXP_PACKSTORE) || defined(QBA_EXP_SMALLNARROW) || defined(QBA_EXP_NOATOMIC) ||          \
-    defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_INTERLEAVE) ||             \
-    defined(QBA_EXP_GRID) || defined(QBA_EXP_NARROW) || defined(QBA_WIDE_QPT) || defined(QBA_MINW) || \
-    defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) || defined(QBA_RED_ALL_IN_FLIGHT) ||           \
-    defined(QBA_QUEUE) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) || defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) || \
-    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N)
+#if defined(QBA_EXP_LDSPAD) || defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||   \
+    defined(QBA_EXP_CHEAPRNG) || defined(QBA_EXP_PADVALU) || defined(QBA_EXP_PADLDS) || defined(QBA_EXP_NOATOMIC) || \
+    defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_GRID) || defined(QBA_EXP_NARROW) ||          \
+    defined(QBA_WIDE_QPT) || defined(QBA_MINW) || defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) ||                \
+    defined(QBA_RED_ALL_IN_FLIGHT) || defined(QBA_QUEUE) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) ||      \
+    defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) ||               \
+    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N) || defined(QBA_PAIRBINS)
 #ifndef QBA_EXPERIMENT_BUILD
 #error "an experiment switch is set without QBA_EXPERIMENT_BUILD (tools/exp/build.sh): not a shippable libqba"
 #endif
@@ -219,6 +218,7 @@ struct qba_ctx {
   // RCCL communicator of the GPU-owner ranks (qba_rccl_init), or null
   void *rccl_comm = nullptr;
   int rccl_ranks = 0;
+  int list_grid = 0;  // > 0: cap on the list kernels' workgroups, no per-workgroup budget (env QBA_LIST_GRID, tests)
 };
 void qba_rccl_release(qba_ctx *ctx);
 

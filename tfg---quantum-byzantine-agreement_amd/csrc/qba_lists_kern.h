@@ -356,27 +356,9 @@ __device__ __forceinline__ void qba_closed_tables(uint32_t rank, const uint32_t 
   asm("" : "+v"(iB));
   uint32_t iC = F::RC > 1 ? (uint32_t)(((uint64_t)(uint32_t)pb * F::RC) >> 32) : 0u;
   if constexpr (F::RC > 1) asm("" : "+v"(iC));
-#ifdef QBA_EXP_NOTABLE
-  A = make_uint4(iA, iA * 3u, iA * 5u, 0u);
-  sB = make_uint2(iB, iB * 7u);
-  sC = iC * 9u;
-#elif defined(QBA_EXP_GTAB)  // experiment builds: stage tables read from global memory (L1 / L2), not LDS
-  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-  typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-  typedef __attribute__((address_space(1))) const v4u GA4;
-  typedef __attribute__((address_space(1))) const v2u GA2;
-  typedef __attribute__((address_space(1))) const uint32_t GA1;
-  const uintptr_t gb = reinterpret_cast<uintptr_t>(pl);
-  const v4u a4 = *reinterpret_cast<GA4 *>(gb + 16 * (uintptr_t)iA);
-  const v2u b2 = *reinterpret_cast<GA2 *>(gb + 4 * (uintptr_t)(F::OFFB + 2 * iB));
-  A = make_uint4(a4.x, a4.y, a4.z, a4.w);
-  sB = make_uint2(b2.x, b2.y);
-  sC = F::RC > 1 ? *reinterpret_cast<GA1 *>(gb + 4 * (uintptr_t)(F::OFFC + iC)) : 0u;
-#else
   A = *reinterpret_cast<const uint4 *>(pl + 4 * iA);
   sB = *reinterpret_cast<const uint2 *>(pl + F::OFFB + 2 * iB);
   sC = F::RC > 1 ? pl[F::OFFC + iC] : 0u;
-#endif
 }
 
 template <int NP>
@@ -759,12 +741,177 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
   if (q.qn >= 64) qba_q_drain<NP, TRUSTED>(q, hist, 64u);
 }
 
+// ---------------------------------------------------------------------------
+// Pair-bin counting (CNT = 1: the fused n = 11 kernel, qba_k_lists MODE 1).
+// The classic histogram takes one ds_add_u32 per counted group per Q entry
+// (11 at n = 11, ~3.5-way bank conflicts each).  Here one atomic counts TWO
+// groups: the bin of a pair (g, h) is (u, L_g, L_h), u = L1, held as an 8-bit
+// lane of a dword:
+//   array A [x_h][u][x_g] dwords (16 KB): lane 0 = pair (2,3), 1 = (4,5),
+//                                         2 = (6,7), 3 = (8,9);
+//   array B, same indexing (16 KB):       lane 0 = pair (10,11); lanes 1-3
+//     (a 24-bit counter, added as 1 << 8) hold group 0 at x_h = u, and the
+//     equal-pair bins C[u][k] at x_g = k & 15, x_h = u ^ (1 + (k >> 4)).
+// The byte address of bin (u, x_g, x_h) is 4 x_g + 64 u + 1024 x_h: with
+// E = values << 2 (byte g = 4 L_g) a 16-bit half of E IS 4 x_g + 1024 x_h
+// for the groups of that half, so each address is ONE v_add_u32 with an SDWA
+// word select onto the entry's row base A + 64 u -- as cheap as the classic
+// per-group address -- and 6 atomics count the 11 groups.  The queue holds an
+// entry as 8 B (c0 = groups 0-3 | groups 4-7 << 4, c1 = groups 8-11): one
+// ds_write_b64 per push and one ds_read_b64 per drain instead of 3 + 3.
+//
+// An 8-bit lane can wrap.  Every Q entry adds exactly one count to every lane
+// and to group 0, so per workgroup each lane's total equals group 0's total
+// (24 bits, exact: a launch gives a workgroup < 2^24 entries) unless a lane
+// wrapped: a wrap loses 256 from its lane and carries at most 1 into the next
+// lane up, so some lane's total then differs from group 0's (the lowest
+// wrapped lane is short by 255 or 256 net, and a lane can only gain what the
+// lane below it lost; B's lane 0 carries into group 0's counter, raising its
+// total, never the lane's).  The flush compares the totals and a workgroup
+// that finds a mismatch recounts its own entries from the rows it stored,
+// with the classic 32-bit bins (qba_lists_body) -- exact in every case.
+// The launcher keeps a workgroup at <= QBA_PB_BUDGET entries per launch, so
+// for sampled lists a wrap needs a bin ~18 sigma above its mean and never
+// happens in practice (tests force it with QBA_LIST_GRID).
+// ---------------------------------------------------------------------------
+#ifndef QBA_PAIRBINS
+#define QBA_PAIRBINS 1
+#endif
+#define QBA_PB_BUDGET (1u << 18)  // entries per workgroup per launch (wrap-free in practice)
+struct QbaPB {
+  static constexpr int WORDS = 8192;       // A [4096] then B [4096]
+  static constexpr int BOFF = 4096;        // B, in words
+  static constexpr int MISC = 8;           // after B: lane totals [0..4], group 0 total [5]
+  static constexpr int AREA = WORDS + MISC;
+  static constexpr int QSLOT = 8;          // queue bytes per entry
+};
+template <int NP, int MODE, int SAMP>
+struct QbaUsePB {  // the fused closed-form n = 11 kernel counts with pair bins
+  static constexpr bool value = QBA_PAIRBINS && NP == 11 && MODE == 1 && SAMP == QBA_S_CLOSED;
+};
+
+// base + 16-bit half h of x in one VALU op (v_add_u32 with an SDWA word select)
+__device__ __forceinline__ uint32_t qba_add_word(uint32_t base, uint32_t x, int h) {
+  uint32_t r;
+  if (h == 0)
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0" : "=v"(r) : "v"(base), "v"(x));
+  else
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "=v"(r) : "v"(base), "v"(x));
+  return r;
+}
+
+__device__ __forceinline__ void qba_lds_add(uint32_t addr, uint32_t v) {
+  atomicAdd((uint32_t *)qba_lds(addr), v);
+}
+
+// Count one Q-correlated entry (c0, c1) into the pair bins; hA = LDS byte
+// address of array A.  Values are the sampler's (< 16), so no range test.
+template <int NP>
+__device__ __forceinline__ void qba_count_pb(uint32_t c0, uint32_t c1, uint32_t hA) {
+  static_assert(NP == 11, "pair bins are laid out for n = 11");
+  constexpr uint32_t B = QbaPB::BOFF * 4;
+  const uint32_t E0 = (c0 << 2) & 0x3c3c3c3cu;  // groups 0-3, x4
+  const uint32_t E1 = (c0 >> 2) & 0x3c3c3c3cu;  // groups 4-7, x4
+  const uint32_t E2 = c1 << 2;                  // groups 8-11, x4
+  const uint32_t hb = (__builtin_amdgcn_ubfe(c0, 8, 4) << 6) + hA;  // A + 64 u
+  qba_lds_add(qba_add_word(hb, E0, 0) + B, 0x100u);      // group 0 at (x_0, u, u), B lanes 1-3
+  qba_lds_add(qba_add_word(hb, E0, 1), 0x1u);            // (2,3)   A lane 0
+  qba_lds_add(qba_add_word(hb, E1, 0), 0x100u);          // (4,5)   A lane 1
+  qba_lds_add(qba_add_word(hb, E1, 1), 0x10000u);        // (6,7)   A lane 2
+  qba_lds_add(qba_add_word(hb, E2, 0), 0x1000000u);      // (8,9)   A lane 3
+  qba_lds_add(qba_add_word(hb, E2, 1) + B, 0x1u);        // (10,11) B lane 0
+  // distinctness (Cond 3 fast path): union of the 12 one-hots, 2 per op
+  const uint32_t one = 0x00010001u;
+  uint32_t U = qba_pk_onehot(c0, one) | qba_pk_onehot(c0 >> 4, one) | qba_pk_onehot(c0 >> 8, one);
+  U |= qba_pk_onehot(c0 >> 12, one) | qba_pk_onehot(c1, one) | qba_pk_onehot(c1 >> 8, one);
+  {
+    uint32_t r;
+    asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
+        : "=v"(r) : "v"(U));
+    U = r;
+  }
+  if (__popc(U) != QCfg<NP>::G) {  // some pair collides: exact slow path (never for sampled lists)
+    const uint32_t w0 = c0 & 0x0f0f0f0fu, w1 = (c0 >> 4) & 0x0f0f0f0fu, w2 = c1;
+    const uint32_t u = __builtin_amdgcn_ubfe(c0, 8, 4);
+    int k = 0;
+#pragma nounroll
+    for (int g = 0; g < QCfg<NP>::G; ++g) {
+      const uint32_t lg = qba_byte_of(g, w0, w1, w2, 0u);
+#pragma nounroll
+      for (int h = g + 1; h < QCfg<NP>::G; ++h, ++k)
+        if (lg == qba_byte_of(h, w0, w1, w2, 0u))
+          qba_lds_add(hA + B + 4 * (uint32_t)((k & 15) + 16 * u + 256 * (u ^ (1 + (k >> 4)))), 0x100u);
+    }
+  }
+}
+
+// the queue's 8-B form of an entry in the byte layout (values < 16)
+template <int NP>
+__device__ __forceinline__ uint2 qba_pb_pack(const uint32_t (&D)[CF<NP>::ND]) {
+  return make_uint2(D[0] | (D[1] << 4), D[2]);
+}
+
+// LDS byte address of pair-bin ring slot s (ring aligned to QBA_QCAP * 8 B)
+__device__ __forceinline__ uint32_t qba_qpb_addr(const QbaWaveQ &q, uint32_t s) {
+  return ((s & (QBA_QCAP - 1)) << 3) | q.base;
+}
+
+template <int NP>
+__device__ __forceinline__ void qba_q_drain_pb(QbaWaveQ &q, uint32_t nv) {
+  const uint32_t lane = __lane_id();
+  typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+  const v2u c = *reinterpret_cast<__attribute__((address_space(3))) v2u *>(
+      static_cast<uintptr_t>(qba_qpb_addr(q, q.tail + lane)));
+  __builtin_amdgcn_s_setprio(2);  // as qba_q_drain
+  if (nv >= 64 || lane < nv) qba_count_pb<NP>(c.x, c.y, q.hoff);
+  __builtin_amdgcn_s_setprio(0);
+  q.tail += nv;
+  q.qn -= nv;
+}
+
+template <int NP>
+__device__ __forceinline__ void qba_q_push_pb(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], bool isq) {
+  const uint64_t m = __ballot(isq);
+  const uint32_t mb = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (isq) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    const uint32_t a = (((mb + q.tail + q.qn) << 3) & (uint32_t)(QBA_QCAP * 8 - 1)) | q.base;
+    const uint2 c = qba_pb_pack<NP>(D);
+    v2u cv;
+    cv.x = c.x;
+    cv.y = c.y;
+    *reinterpret_cast<__attribute__((address_space(3))) v2u *>(static_cast<uintptr_t>(a)) = cv;
+  }
+  q.qn += (uint32_t)__popcll(m);
+  if (q.qn >= 64) qba_q_drain_pb<NP>(q, 64u);
+}
+
+// Push (the wave queue) / count one entry directly (tails) with the counting
+// scheme CNT (0: classic 32-bit bins in `hist`, 1: pair bins, hist = array A).
+template <int NP, bool TRUSTED, int CNT>
+__device__ __forceinline__ void qba_push(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], bool isq, uint32_t *hist) {
+  if constexpr (CNT == 1)
+    qba_q_push_pb<NP>(q, D, isq);
+  else
+    qba_q_push<NP, TRUSTED>(q, D, isq, hist);
+}
+template <int NP, int CNT>
+__device__ __forceinline__ void qba_count_one(const uint32_t (&D)[CF<NP>::ND], uint32_t *hist) {
+  if constexpr (CNT == 1) {
+    if ((D[0] & 0xffu) == ((D[0] >> 8) & 0xffu)) return;  // not Q-correlated (tfg.py:327)
+    const uint2 c = qba_pb_pack<NP>(D);
+    qba_count_pb<NP>(c.x, c.y, (uint32_t)(uintptr_t)(qba_lds_u32 *)hist);
+  } else {
+    qba_count_d<NP>(D, 0x00010001u, hist, true);
+  }
+}
+
 // One thread-step over QPT consecutive quads: entries [c0, c0 + 4 QPT) of the
 // launch (columns of `lists`).  Each list row is stored / loaded as one
 // 4*QPT-byte vector per thread (16 B at QPT = 4: a wave moves 1 KiB per row).
 // MODE 0: sample -> lists;  MODE 1: sample -> lists + counts;  MODE 2: lists -> counts
 // TAIL (QPT = 1 only): the last, partial quad, byte by byte.
-template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false>
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false, int CNT = 0>
 __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                          uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                          const uint64_t *pat, const uint64_t *apat,
@@ -775,6 +922,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
   constexpr int ND = CF<NP>::ND;
   static_assert(QPT == 1 || QPT == 2 || QPT == 4, "QPT");
   static_assert(!TAIL || QPT == 1, "tail quads are single");
+  static_assert(CNT == 0 || MODE == 1, "pair bins count the fused kernel's own lists only");
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   using V = typename std::conditional<QPT == 4, u32x4, typename std::conditional<QPT == 2, u32x2, uint32_t>::type>::type;
@@ -826,7 +974,11 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
           // row 0 XOR row 1 is nonzero iff entry j is Q-correlated
           const uint32_t xq = (row[k][0] ^ row[k][1]) & (act ? 0xffffffffu : 0u);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) qba_q_push<NP, MODE == 1>(*wq, D[j], (xq & (0xffu << (8 * j))) != 0u, hist);
+          for (int j = 0; j < 4; ++j) qba_push<NP, MODE == 1, CNT>(*wq, D[j], (xq & (0xffu << (8 * j))) != 0u, hist);
+        } else if constexpr (CNT == 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < valid) qba_count_one<NP, 1>(D[j], hist);
         } else {
           qba_count_quad<NP>(D, valid, hist, row[k]);
         }
@@ -850,22 +1002,6 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
       for (int i = 0; i < QBA_EXP_PADLDS; ++i) z ^= reinterpret_cast<volatile uint32_t *>(hist)[4 * i];
       asm volatile("" ::"v"(z));
     }
-#endif
-#ifdef QBA_EXP_PACKSTORE  // experiment builds: rows stored as packed nibbles (half the bytes; layout wrong by design)
-    if constexpr (QPT == 2) {
-      if (!TAIL && act) {
-#pragma unroll
-        for (int g = 0; g < C::G; ++g) {
-          uint64_t rb = reinterpret_cast<uint64_t>(lists) + (uint64_t)g * ld;
-          asm("" : "+s"(rb));
-          typedef __attribute__((address_space(1))) uint32_t GU;
-          __builtin_nontemporal_store(row[0][g] | (row[1][g] << 4), reinterpret_cast<GU *>(rb + (c0 >> 1)));
-        }
-      } else if (TAIL) {
-        for (int g = 0; g < C::G; ++g)
-          for (int j = 0; j < valid; ++j) lists[(uint64_t)g * ld + c0 + j] = (uint8_t)(row[0][g] >> (8 * j));
-      }
-    } else
 #endif
 #ifdef QBA_EXP_NOSTORE
     if (row[0][0] == 0x12345678u && row[0][1] == 0x9abcdef0u)
@@ -913,7 +1049,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
 // QPT = 1 (unaligned starts, the tail quads): 2 bytes per row, stored as bytes
 // (a chunk may start at an odd byte).  MODE 2 reads the same layout; an
 // unpacked quad's entries come out permuted (counting is order-free).
-template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false>
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false, int CNT = 0>
 __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                             uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                             const uint64_t *pat, const uint64_t *apat,
@@ -924,6 +1060,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
   constexpr int ND = CF<NP>::ND;
   static_assert(QPT == 1 || QPT == 2, "packed rows: QPT 1 or 2");
   static_assert(!TAIL || QPT == 1, "tail quads are single");
+  static_assert(CNT == 0 || MODE == 1, "pair bins count the fused kernel's own lists only");
   static_assert(C::W <= 16, "a value must fit a nibble");
   typedef __attribute__((address_space(1))) uint32_t GU;
   const int valid = !TAIL ? 4 : ((count - c0) >= 4 ? 4 : (int)(count - c0));
@@ -988,13 +1125,13 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
           for (int p = 0; p < 2; ++p) {
             const uint32_t w0 = Dp[2 * k + p][0];
             const uint32_t x = (w0 ^ (w0 >> 8)) & am;
-            qba_q_push<NP, true>(*wq, D[2 * p], (x & 0x0fu) != 0u, hist);
-            qba_q_push<NP, true>(*wq, D[2 * p + 1], x > 0x0fu, hist);
+            qba_push<NP, true, CNT>(*wq, D[2 * p], (x & 0x0fu) != 0u, hist);
+            qba_push<NP, true, CNT>(*wq, D[2 * p + 1], x > 0x0fu, hist);
           }
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (j < valid) qba_count_d<NP>(D[j], 0x00010001u, hist, true);
+            if (j < valid) qba_count_one<NP, CNT>(D[j], hist);
         }
       }
     }
@@ -1057,7 +1194,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
   }
 }
 
-template <int NP, int MODE, int SAMP, int QPT, bool TAIL, int PK, bool WQ = false>
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, int PK, bool WQ = false, int CNT = 0>
 __device__ __forceinline__ void qba_step_l(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                            uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                            const uint64_t *pat, const uint64_t *apat,
@@ -1065,9 +1202,9 @@ __device__ __forceinline__ void qba_step_l(uint32_t c0, uint32_t count, uint64_t
                                            uint8_t *__restrict__ lists, uint64_t ld, uint32_t *hist,
                                            QbaWaveQ *wq = nullptr, bool act = true) {
   if constexpr (PK)
-    qba_step_pk<NP, MODE, SAMP, QPT, TAIL, WQ>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
+    qba_step_pk<NP, MODE, SAMP, QPT, TAIL, WQ, CNT>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
   else
-    qba_step<NP, MODE, SAMP, QPT, TAIL, WQ>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
+    qba_step<NP, MODE, SAMP, QPT, TAIL, WQ, CNT>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
 }
 
 // Stage the program's tables in LDS; returns the histogram base after them.
@@ -1078,11 +1215,6 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   pat = apat = thr = lds;
   pl = reinterpret_cast<const uint32_t *>(lds);
   uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
-#ifdef QBA_EXP_GTAB
-  if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
-    pl = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
-  } else
-#endif
   if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
@@ -1132,6 +1264,78 @@ __device__ __forceinline__ void qba_zero_outputs(const QbaZero &z, int tid, int 
   if ((z.flags & 2) && z.stats && tid < C::STATS) z.stats[tid] = 0;
 }
 
+// The pair bins' flush: the classic slab row (H [u][g][x] as counted, the
+// pair bins C[u][k], the stats) from the marginals of arrays A / B, after the
+// wrap test (see QbaPB).  Returns true -- for every thread -- when a lane
+// wrapped; the slab row is then left to the caller's recount.  Slab words of
+// group 1 and the row padding are not written (the reductions skip them).
+template <int NP, int BS>
+__device__ __forceinline__ bool qba_pb_flush(uint32_t *hist, uint32_t *row) {
+  using C = QCfg<NP>;
+  static_assert(BS >= 512, "four roles of 256 threads");
+  const uint32_t *A = hist, *Bw = hist + QbaPB::BOFF;
+  uint32_t *misc = hist + QbaPB::WORDS;
+  const int t = threadIdx.x;
+  uint32_t v[5] = {0u, 0u, 0u, 0u, 0u}, g0 = 0u;
+  const int ug = (t & 255) >> 4, xg = t & 15;    // column-sum threads: (u, x)
+  const int ur = t & 15, yr = (t & 255) >> 4;    // row-sum threads: (u, y), u fastest
+  if (t < 256) {  // groups 2, 4, 6, 8, 10 (x_g of each pair): sums over x_h
+    uint32_t s02 = 0u, s13 = 0u, sb = 0u;
+    const uint32_t *a = A + xg + 16 * ug, *b = Bw + xg + 16 * ug;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t d = a[256 * k];
+      s02 += d & 0x00ff00ffu;
+      s13 += (d >> 8) & 0x00ff00ffu;
+      sb += b[256 * k] & 0xffu;
+    }
+    v[0] = s02 & 0xffffu;  // (2,3)
+    v[1] = s13 & 0xffffu;  // (4,5)
+    v[2] = s02 >> 16;      // (6,7)
+    v[3] = s13 >> 16;      // (8,9)
+    v[4] = sb;             // (10,11)
+    g0 = Bw[xg + 16 * ug + 256 * ug] >> 8;
+#pragma unroll
+    for (int p = 0; p < 5; ++p) atomicAdd(&misc[p], v[p]);
+    atomicAdd(&misc[5], g0);
+  } else if (t < 512) {  // groups 3, 5, 7, 9, 11 (x_h of each pair): sums over x_g
+    uint32_t s02 = 0u, s13 = 0u, sb = 0u;
+    const uint4 *a = reinterpret_cast<const uint4 *>(A + 16 * ur + 256 * yr);
+    const uint4 *b = reinterpret_cast<const uint4 *>(Bw + 16 * ur + 256 * yr);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 d = a[(k + ur) & 3], e = b[(k + ur) & 3];  // rotated: fewer bank conflicts
+      s02 += (d.x & 0x00ff00ffu) + (d.y & 0x00ff00ffu) + (d.z & 0x00ff00ffu) + (d.w & 0x00ff00ffu);
+      s13 += ((d.x >> 8) & 0x00ff00ffu) + ((d.y >> 8) & 0x00ff00ffu) + ((d.z >> 8) & 0x00ff00ffu) +
+             ((d.w >> 8) & 0x00ff00ffu);
+      sb += (e.x & 0xffu) + (e.y & 0xffu) + (e.z & 0xffu) + (e.w & 0xffu);
+    }
+    v[0] = s02 & 0xffffu;
+    v[1] = s13 & 0xffffu;
+    v[2] = s02 >> 16;
+    v[3] = s13 >> 16;
+    v[4] = sb;
+  }
+  __syncthreads();
+  const bool wrap = misc[0] != misc[5] || misc[1] != misc[5] || misc[2] != misc[5] || misc[3] != misc[5] ||
+                    misc[4] != misc[5];
+  if (wrap) return true;  // workgroup-uniform
+  if (t < 256) {
+    row[(ug * C::G + 0) * C::WP + xg] = g0;
+#pragma unroll
+    for (int p = 0; p < 5; ++p) row[(ug * C::G + 2 + 2 * p) * C::WP + xg] = v[p];
+  } else if (t < 512) {
+#pragma unroll
+    for (int p = 0; p < 5; ++p) row[(ur * C::G + 3 + 2 * p) * C::WP + yr] = v[p];
+  }
+  for (int i = t; i < C::CBL; i += BS) {  // C[u][k]: B lanes 1-3 at (k & 15, u, u ^ (1 + k / 16))
+    const int u = i / C::CP, k = i - u * C::CP;
+    row[C::HBL + i] = Bw[(k & 15) + 16 * u + 256 * (u ^ (1 + (k >> 4)))] >> 8;
+  }
+  if (t < C::STATS) row[C::HBL + C::CBL + t] = 0u;  // sampled values are < w
+  return false;
+}
+
 // Waves per SIMD the list kernels are compiled for.  The closed-form sampler
 // runs 2 workgroups of 1024 threads per CU = 8 waves per SIMD (the CDNA4
 // maximum): with its quads sampled pair by pair (QBA_PAIRWISE) and the round
@@ -1149,7 +1353,7 @@ __device__ __forceinline__ void qba_zero_outputs(const QbaZero &z, int tid, int 
 // PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row.
 // The body of the list kernel; its workgroups are those after the first
 // `red` (qba_k_lists: 0; qba_k_lists_def: its reduce workgroups).
-template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK>
+template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK, int CNT = 0>
 __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1,
                                                uint64_t first, uint32_t count, uint8_t *__restrict__ lists,
                                                uint64_t ld, uint32_t *__restrict__ slab, QbaZero zero,
@@ -1165,7 +1369,8 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
 #endif
   uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
   if (MODE != 0) {
-    for (int i = threadIdx.x; i < C::NBP; i += BS) hist[i] = 0u;
+    constexpr int NZ = CNT ? QbaPB::AREA : C::NBP;
+    for (int i = threadIdx.x; i < NZ; i += BS) hist[i] = 0u;
 #if !QBA_ZERO_AT_END
     if (bid == 0) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
 #endif
@@ -1182,36 +1387,32 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   // scalar load whose s_waitcnt lgkmcnt(0) also drains every LDS atomic the
   // wave has in flight (-2% step time)
   const uint32_t ustride = __builtin_amdgcn_readfirstlane(nblk * BS);
-#ifdef QBA_EXP_INTERLEAVE  // experiment builds: waves interleaved across workgroups
-  const uint32_t u0 = ((threadIdx.x >> 6) * nblk + bid) * 64 + (threadIdx.x & 63);
-#else
   const uint32_t u0 = bid * BS + threadIdx.x;
-#endif
   if constexpr (MODE != 0 && QBA_QUEUE) {
     QbaWaveQ wq;
-    wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
+    if constexpr (CNT) {  // 8-B slots after the pair bins, each ring aligned to its size
+      const uint32_t h = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist + QbaPB::AREA * 4;
+      wq.base = ((h + QBA_QCAP * 8 - 1) & ~(uint32_t)(QBA_QCAP * 8 - 1)) + (threadIdx.x >> 6) * (QBA_QCAP * 8);
+    } else {
+      wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
+    }
     wq.tail = 0;
     wq.qn = 0;
     wq.hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     asm("" : "+v"(wq.hoff));  // held in a VGPR (no instruction is emitted)
-#ifdef QBA_EXP_DESYNC  // experiment builds: stagger the waves' phase at the start (s_sleep units of 64 cycles)
-    switch ((threadIdx.x >> 6) % 6) {
-      case 1: __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
-      case 2: __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
-      case 3: for (int i = 0; i < 3; ++i) __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
-      case 4: for (int i = 0; i < 4; ++i) __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
-      case 5: for (int i = 0; i < 5; ++i) __builtin_amdgcn_s_sleep(QBA_EXP_DESYNC); break;
-      default: break;
-    }
-#endif
     // wave-uniform trip count: pushes and drains always run with the whole wave
     for (uint32_t u = u0;; u += ustride) {
       const bool act = u < nunits;
       if (!__any(act)) break;
-      qba_step_l<NP, MODE, SAMP, QPT, false, PK, true>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
-                                                 lists, ld, hist, &wq, act);
+      qba_step_l<NP, MODE, SAMP, QPT, false, PK, true, CNT>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr,
+                                                            pl, lists, ld, hist, &wq, act);
     }
-    while (wq.qn) qba_q_drain<NP, MODE == 1>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
+    while (wq.qn) {  // wave-uniform
+      if constexpr (CNT)
+        qba_q_drain_pb<NP>(wq, wq.qn < 64 ? wq.qn : 64u);
+      else
+        qba_q_drain<NP, MODE == 1>(wq, hist, wq.qn < 64 ? wq.qn : 64u);
+    }
   } else {
     for (uint32_t u = u0; u < nunits; u += ustride)
       qba_step_l<NP, MODE, SAMP, QPT, false, PK>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
@@ -1222,19 +1423,49 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   if (!(QBA_EXP_SKIP & 1) && bid == nblk - 1 && threadIdx.x < rq) {
     const uint32_t c0 = r0 + 4 * threadIdx.x;
     if (c0 + 4 <= count)
-      qba_step_l<NP, MODE, SAMP, 1, false, PK>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
+      qba_step_l<NP, MODE, SAMP, 1, false, PK, false, CNT>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
     else
-      qba_step_l<NP, MODE, SAMP, 1, true, PK>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
+      qba_step_l<NP, MODE, SAMP, 1, true, PK, false, CNT>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
   }
   if (MODE != 0) {
     __syncthreads();
 #ifdef QBA_EXP_TIMING
     const uint64_t ts2 = wall_clock64();
 #endif
-    uint4 *dst = reinterpret_cast<uint4 *>(slab + (size_t)bid * C::NBP);
-    const uint4 *src = reinterpret_cast<const uint4 *>(hist);
-    if (!(QBA_EXP_SKIP & 2))
+    uint32_t *row = slab + (size_t)bid * C::NBP;
+    bool classic = !CNT;
+    if constexpr (CNT) {
+      if (!(QBA_EXP_SKIP & 2) && qba_pb_flush<NP, BS>(hist, row)) {
+        // a pair-bin lane wrapped (never for sampled lists at QBA_PB_BUDGET
+        // entries per workgroup): recount this workgroup's entries -- the
+        // same units and tail as above -- from the rows it stored, into the
+        // classic 32-bit bins (qba_count_quad: exact, order-free)
+        __syncthreads();
+        for (int i = threadIdx.x; i < C::NBP; i += BS) hist[i] = 0u;
+        __threadfence();  // this workgroup's list stores are complete and visible to its loads
+        __syncthreads();
+        for (uint32_t u = u0; u < nunits; u += ustride)
+          qba_step_l<NP, 2, QBA_S_GENERAL, QPT, false, PK>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr,
+                                                         pl, lists, ld, hist);
+        if (bid == nblk - 1 && threadIdx.x < rq) {
+          const uint32_t c0 = r0 + 4 * threadIdx.x;
+          if (c0 + 4 <= count)
+            qba_step_l<NP, 2, QBA_S_GENERAL, 1, false, PK>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists,
+                                                         ld, hist);
+          else
+            qba_step_l<NP, 2, QBA_S_GENERAL, 1, true, PK>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists,
+                                                        ld, hist);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) hist[C::HBL + C::CBL + 1] += 1u;  // stats[1]: recounting workgroups
+        classic = true;
+      }
+    }
+    if (classic && !(QBA_EXP_SKIP & 2)) {
+      uint4 *dst = reinterpret_cast<uint4 *>(row);
+      const uint4 *src = reinterpret_cast<const uint4 *>(hist);
       for (int i = threadIdx.x; i < C::NBP / 4; i += BS) dst[i] = src[i];
+    }
 #ifdef QBA_EXP_TIMING
     if (threadIdx.x == 0) {
       tsl[0] = ts0;
@@ -1258,7 +1489,8 @@ __global__ void QBA_LISTS_BOUNDS
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                 uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
                 uint32_t *__restrict__ slab, QbaZero zero) {
-  qba_lists_body<NP, MODE, SAMP, QPT, PK>(ps, k0, k1, first, count, lists, ld, slab, zero, 0u);
+  qba_lists_body<NP, MODE, SAMP, QPT, PK, QBA_LBLOCK, QbaUsePB<NP, MODE, SAMP>::value ? 1 : 0>(
+      ps, k0, k1, first, count, lists, ld, slab, zero, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -1646,7 +1878,11 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     if (int rc = check_closed<NP>(hs)) return rc;
     lds += table_lds<NP>(hs, samp);
   }
-  if (L.mode != 0) {
+  // the fused closed-form kernel counts with pair bins (QbaPB)
+  const bool pb = QbaUsePB<NP, 1, QBA_S_CLOSED>::value && L.mode == 1 && samp == QBA_S_CLOSED;
+  if (pb) {
+    lds += (size_t)QbaPB::AREA * sizeof(uint32_t) + (size_t)(QBA_LBLOCK / 64 + 1) * QBA_QCAP * QbaPB::QSLOT;
+  } else if (L.mode != 0) {
     lds += (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
     if (QBA_QUEUE) lds += (size_t)(QBA_LBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
   }
@@ -1660,18 +1896,13 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   const bool wide = false;
 #else
   constexpr uintptr_t VA = 4 * QBA_WIDE_QPT - 1;  // row vectors need their natural alignment
-#ifdef QBA_EXP_SMALLNARROW  // experiment builds: launches below this many entries take the narrow kernel on a wider grid
-  const bool small = L.count < (uint64_t)QBA_EXP_SMALLNARROW;
-#else
-  // (the one-quad step on twice the workgroups shortens a small launch's list
-  // kernel -- 8.8 vs 10.1 us at 1e6 entries -- but its workgroups then share
-  // CUs with the deferred reduction's: 11.7 vs 10.3 us per configs[1] step,
-  // profiles/r3/r3m, r3n; not taken)
-  const bool small = false;
-#endif
+  // (the one-quad step on twice the workgroups for small launches shortens
+  // the list kernel -- 8.8 vs 10.1 us at 1e6 entries -- but its workgroups
+  // then share CUs with the deferred reduction's: 11.7 vs 10.3 us per
+  // configs[1] step, profiles/r3/r3m, r3n; not taken, tools/exp/rejected)
   // nibble rows: the wide step stores one 4-B word per row (QPT = 2)
   const uintptr_t va = L.packed ? 3 : VA;
-  const bool wide = !small && !(reinterpret_cast<uintptr_t>(L.lists) & va) && !(L.ld & va);
+  const bool wide = !(reinterpret_cast<uintptr_t>(L.lists) & va) && !(L.ld & va);
 #endif
 #define QBA_K(M, S)                                                                          \
   (L.packed ? (wide ? (const void *)qba_k_lists<NP, M, S, 2, 1> : (const void *)qba_k_lists<NP, M, S, 1, 1>) \
@@ -1692,7 +1923,26 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
 #undef QBA_K
   if (lds > 65536) QBA_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int cap = 0;
-  const int grid = grid_for(ctx, kern, lds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1, &cap);
+  int grid = grid_for(ctx, kern, lds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1, &cap);
+  if (ctx->list_grid > 0 && grid > ctx->list_grid) grid = ctx->list_grid;  // tests (QBA_LIST_GRID)
+  if (pb && !ctx->list_grid && L.count > (uint64_t)cap * QBA_PB_BUDGET) {
+    // at most QBA_PB_BUDGET entries per workgroup and launch (QbaPB): later
+    // parts accumulate; part boundaries are multiples of 2^18 entries, so the
+    // row alignment and the pair parity of `first` are those of the call
+    const uint64_t part = (uint64_t)cap * QBA_PB_BUDGET;
+    QbaLaunch S = L;
+    S.defer = 0;
+    int rc = QBA_OK;
+    for (uint64_t done = 0; !rc && done < L.count; done += S.count) {
+      S.count = L.count - done < part ? L.count - done : part;
+      S.first = L.first + done;
+      S.lists = L.lists + (L.packed ? done >> 1 : done);
+      S.accumulate = done ? 1 : L.accumulate;
+      S.stats_accumulate = done ? 1 : L.stats_accumulate;
+      rc = qba_launch_lists<NP>(ctx, S);
+    }
+    return rc;
+  }
   const uint32_t k0 = (uint32_t)L.seed, k1 = (uint32_t)(L.seed >> 32);
   const QbaProgramSet *ps = L.ps;
   uint64_t first = L.first;

@@ -29,6 +29,12 @@ for f in root.glob("p*/**/*counter_collection.csv"):
         if r["Kernel_Name"].startswith(f"void qba_k_lists<{n}, 1"):
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 fetch = statistics.median(vals["FETCH_SIZE"]) * 1024 * 2
+# the issue side of the same kernel (the other tools/pmc.sh passes): per-launch
+# medians, summed over the chip; bench.py turns them into roofline.issue
+ISSUE = ("GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_LDS_ATOMIC", "SQ_INSTS_SALU",
+         "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+         "SQ_INSTS_VMEM_WR")
+issue = {c: statistics.median(vals[c]) for c in ISSUE if c in vals}
 write = statistics.median(vals["WRITE_SIZE"]) * 1024
 known = (n + 1) * per // (2 if layout == "packed" else 1)
 out = {"n": n, "per_launch_entries": per, "mode": mode, "layout": layout,
@@ -36,6 +42,7 @@ out = {"n": n, "per_launch_entries": per, "mode": mode, "layout": layout,
        "write_calibration": {"known_list_bytes": known, "write_over_known": write / known},
        "algorithmic_bytes_per_launch": 2 * (n + 1) * per,
        "source": str(root), "kernel": f"qba_k_lists<{n},1,*>",
+       "issue_counters_per_launch": issue,
        # the library the counters were read from: bench.py drops the figure for any other build
        "libqba_sha16": hashlib.sha256(open(os.environ.get("QBA_LIB", Path(__file__).resolve().parent.parent
                                                          / "tfg---quantum-byzantine-agreement_amd" / "_build"
