@@ -181,7 +181,16 @@ QBA_API int qba_sample_check_deferred(qba_ctx *ctx, int n_parties, uint64_t seed
 QBA_API int qba_sample_check_packed_deferred(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
                                              uint64_t count, uint8_t *packed_dev, uint64_t ld, int64_t *H_dev,
                                              int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);
-/* Launches the pending deferred reduction (if any) on its call's stream. */
+/* Launches the pending deferred reduction (if any) on its call's stream.
+ * Graph capture: a deferred reduction must be launched in the capture state
+ * it was recorded in, so call qba_flush_deferred before beginning a capture
+ * and before ending one (the deferred calls inside a capture then form a
+ * closed chain).  A call that would carry a pending reduction across a
+ * capture boundary fails with QBA_ESTATE; qba_flush_deferred outside the
+ * capture of a captured pending reduction drops it (QBA_ESTATE: that call's
+ * counts stay incomplete).  Counting calls of one ctx on different streams
+ * are ordered by an event on the shared scratch (qba_last_stats and
+ * qba_destroy flush a pending reduction first). */
 QBA_API int qba_flush_deferred(qba_ctx *ctx);
 /* Rows [0, rows) of `count` columns between the layouts.  pack: *bad_dev (may
  * be NULL) receives how many values were > 15 (stored as value & 15). */

@@ -172,3 +172,38 @@ def test_deferred_stats(engine):
     engine.flush_deferred()
     torch.cuda.synchronize()
     assert list(engine.last_stats()) == [0, 0]
+
+
+def test_deferred_capture_boundaries(engine):
+    """a pending deferred reduction never crosses a capture
+    boundary.  (a) pending from before a capture -> the deferred call inside
+    the capture fails with QBA_ESTATE; (b) pending at the end of a capture ->
+    qba_flush_deferred outside fails and drops it; the ctx stays usable and
+    the next eager calls are exact."""
+    qe = sub("_lib").QbaError
+    n, count = 11, 50_000
+    packed = engine.alloc_packed(n, count)
+    c = engine.alloc_counts(n)
+    engine.sample_check_packed(n, 3, 0, count, packed, c, deferred=True)  # pending, eager
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(qe):
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                engine.sample_check_packed(n, 4, 0, count, packed, c, deferred=True)
+    engine.flush_deferred()  # the eager pending one, eagerly
+    torch.cuda.synchronize()
+    assert _eq(c, _ref_counts(engine, n, 3, 0, count))
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g2, stream=s):
+            engine.sample_check_packed(n, 5, 0, count, packed, c, deferred=True)  # left pending
+    with pytest.raises(qe):
+        engine.flush_deferred()
+    c2 = engine.alloc_counts(n)
+    engine.sample_check_packed(n, 6, 0, count, packed, c2, deferred=True)
+    engine.flush_deferred()
+    torch.cuda.synchronize()
+    assert _eq(c2, _ref_counts(engine, n, 6, 0, count))
+    assert list(engine.last_stats()) == [0, 0]

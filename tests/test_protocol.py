@@ -35,10 +35,19 @@ def _compare(run, want):
     assert run.bytes == want["bytes"]
 
 
-def _run(engine, case):
+def _run(engine, case, **party_kwargs):
     protocol = sub("protocol")
     return protocol.run_local(case["n"], case["sizeL"], case["nDishonest"], engine,
-                              seed=case["seed"], lists=LISTS[case["name"]], timeout=60)
+                              seed=case["seed"], lists=LISTS[case["name"]], timeout=60,
+                              party_kwargs=party_kwargs or None)
+
+
+class _RowEngine(OracleEngine):
+    """The numpy oracle engine presenting itself as a device engine (it has
+    lists_to_bits), so an in-process run takes the device-row list sends."""
+
+    def lists_to_bits(self, *a):  # pragma: no cover - never called on the device-row path
+        raise AssertionError("the device-row path must not encode lists")
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
@@ -46,10 +55,27 @@ def test_protocol_exact_cpu_host(case):
     _compare(_run(OracleEngine(), case), case["exact"])
 
 
+@pytest.mark.parametrize("case", CASES[::6], ids=[c["name"] for c in CASES[::6]])
+def test_protocol_exact_device_rows_cpu_host(case):
+    """In-process runs hand each rank its list row (comm.DeviceRow) instead of
+    the int64-per-bit wire encoding; decisions, V_i, accept/reject, sends and
+    the accounted messages / bytes stay the fixtures'."""
+    _compare(_run(_RowEngine(), case), case["exact"])
+
+
 @pytest.mark.gpu
 def test_protocol_exact_gpu(engine):
+    """The product path in-process: device rows, no wire codec."""
     for case in CASES:
         _compare(_run(engine, case), case["exact"])
+
+
+@pytest.mark.gpu
+def test_protocol_exact_gpu_wire(engine):
+    """The same fixtures with the reference's wire layout for the lists
+    (tfg.py:142-161, the --wire / mpiexec form)."""
+    for case in CASES:
+        _compare(_run(engine, case, wire=True), case["exact"])
 
 
 def test_consistent_host_kat():
@@ -152,3 +178,33 @@ def test_protocol_python_sets_path(name, monkeypatch):
     monkeypatch.setattr(protocol, "NATIVE_SETS", False)
     case = next(c for c in CASES if c["name"] == name)
     _compare(_run(OracleEngine(), case), case["exact"])
+
+
+def test_local_world_device_row_messages():
+    """comm.DeviceRow through a LocalWorld: delivered by reference into a
+    RowSlot, accounted as its wire message (size items x 8 B), truncation and
+    a plain-buffer receive refused."""
+    comm = sub("comm")
+    w = comm.LocalWorld(2, coop=False)
+    row = np.arange(10, dtype=np.uint8)
+
+    def body(c):
+        if c.rank == 0:
+            c.Send([comm.DeviceRow(row, 30), None], dest=1)
+            return None
+        slot = comm.RowSlot(30)
+        c.Recv([slot, None], source=0)
+        return slot.row
+
+    res = w.run(body)
+    assert res[1] is row and w.sent_messages == 1 and w.sent_bytes == 240
+    w2 = comm.LocalWorld(2, coop=False, timeout=5)
+
+    def bad(c):
+        if c.rank == 0:
+            c.Send([comm.DeviceRow(row, 31), None], dest=1)
+            return None
+        c.Recv([comm.RowSlot(30), None], source=0)
+
+    with pytest.raises(Exception):
+        w2.run(bad)

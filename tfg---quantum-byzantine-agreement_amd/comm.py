@@ -61,8 +61,33 @@ class Status:
         return self.tag
 
 
-def _payload(buf) -> np.ndarray:
+class DeviceRow:
+    """In-process payload of one of rank 0's list sends (tfg.py:142-161): the
+    device row itself instead of the reference's one-int64-per-bit encoding
+    of it.  It is accounted as the wire message it stands for -- ``nbytes``
+    and ``size`` of the rawS row -- so a LocalWorld run reports the same
+    messages and bytes as the wire run.  Received only into a RowSlot."""
+
+    __slots__ = ("row", "nbytes", "size")
+
+    def __init__(self, row, size: int, itemsize: int = 8):
+        self.row, self.size, self.nbytes = row, int(size), int(size) * itemsize
+
+
+class RowSlot:
+    """Receive buffer of a DeviceRow message (``size`` wire items, as the
+    np.empty(nq * sizeL) buffer it replaces); ``row`` after delivery."""
+
+    __slots__ = ("row", "size")
+
+    def __init__(self, size: int):
+        self.row, self.size = None, int(size)
+
+
+def _payload(buf):
     arr = buf[0] if isinstance(buf, (list, tuple)) else buf
+    if isinstance(arr, DeviceRow):
+        return arr
     return np.array(arr, copy=True)
 
 
@@ -88,6 +113,15 @@ def _matches(want_src, want_tag, src, tag) -> bool:
 
 def _deliver(post: _Posted, msg: _Msg) -> None:
     dst = post.buf[0] if isinstance(post.buf, (list, tuple)) else post.buf
+    if isinstance(msg.data, DeviceRow) or isinstance(dst, RowSlot):
+        if not (isinstance(msg.data, DeviceRow) and isinstance(dst, RowSlot)):
+            raise TypeError("a device-row message is received into a RowSlot (and only such a message)")
+        if msg.data.size > dst.size:
+            raise RuntimeError(f"message truncated: {msg.data.size} items into a buffer of {dst.size}")
+        dst.row = msg.data.row
+        post.status.source, post.status.tag = msg.src, msg.tag
+        post.done = True
+        return
     flat = dst.reshape(-1)
     src = msg.data.reshape(-1)
     if src.size > flat.size:

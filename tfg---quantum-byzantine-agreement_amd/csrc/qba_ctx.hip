@@ -60,9 +60,14 @@ extern "C" int qba_init(int device, qba_ctx **out) {
   return QBA_OK;
 }
 
+// qba_lists.hip; absent from the host-only sanitizer build (no list kernels)
+extern "C" __attribute__((weak)) int qba_flush_deferred(qba_ctx *ctx);
+
 extern "C" int qba_destroy(qba_ctx *ctx) {
   if (!ctx) return QBA_OK;
   (void)hipSetDevice(ctx->device);
+  // a pending deferred reduction completes its call's counts before the slab goes
+  if (ctx->pend.flush && qba_flush_deferred && qba_flush_deferred(ctx) == QBA_OK) (void)hipDeviceSynchronize();
   qba_rccl_release(ctx);
   for (int n = 0; n <= QBA_MAX_PARTIES; ++n) {
     if (ctx->prog_dev[n]) (void)hipFree(ctx->prog_dev[n]);
@@ -141,6 +146,7 @@ extern "C" int qba_last_stats(qba_ctx *ctx, int64_t *out2) {
   if (!ctx || !out2) return qba_fail(QBA_EINVAL, "qba_last_stats: bad arguments");
   int rc = qba_set_device(ctx);
   if (rc) return rc;
+  if (qba_flush_deferred && (rc = qba_flush_deferred(ctx))) return rc;  // the last call's stats follow its reduction
   QBA_HIP(hipDeviceSynchronize());
   QBA_HIP(hipMemcpy(out2, ctx->stats, 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
   return QBA_OK;

@@ -219,7 +219,20 @@ struct qba_ctx {
   void *rccl_comm = nullptr;
   int rccl_ranks = 0;
   int list_grid = 0;  // > 0: cap on the list kernels' workgroups, no per-workgroup budget (env QBA_LIST_GRID, tests)
+  // graph capture of the pending deferred reduction (pend): 1 when it was
+  // recorded inside a capture, with that capture's id
+  int pend_captured = 0;
+  unsigned long long pend_capture_id = 0;
+  // the stream of the slab's last user (qba_slab_order): a counting launch on
+  // another stream is ordered after it
+  hipStream_t slab_stream = nullptr;
+  bool slab_used = false;
 };
+// Capture state of a stream: 1 capturing (its capture id in *id), 0 not.
+int qba_capture_of(hipStream_t s, unsigned long long *id);
+// Order a counting launch on `stream` after the slab's previous user on
+// another stream (an event, or nothing when that stream is idle).
+int qba_slab_order(qba_ctx *ctx, hipStream_t stream);
 void qba_rccl_release(qba_ctx *ctx);
 
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes);

@@ -145,9 +145,54 @@ static int dispatch(qba_ctx *ctx, const QbaLaunch &L0) {
   return rc;
 }
 
+int qba_capture_of(hipStream_t s, unsigned long long *id) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  if (hipStreamGetCaptureInfo(s, &st, &cid) != hipSuccess) st = hipStreamCaptureStatusNone;
+  *id = st == hipStreamCaptureStatusActive ? cid : 0ull;
+  return st == hipStreamCaptureStatusActive ? 1 : 0;
+}
+
+// A pending deferred reduction may only be launched in the capture state it
+// was recorded in: an eager one into an eager stream, a captured one into the
+// same capture.  Otherwise the reduction would become a graph node that
+// re-reduces an overwritten slab on every replay, or an eager launch would
+// reduce the slab of a graph that has not run (include/qba.h).
+static int pend_capture_ok(qba_ctx *ctx, hipStream_t s) {
+  unsigned long long id = 0;
+  const int cap = qba_capture_of(s, &id);
+  if (cap == ctx->pend_captured && (!cap || id == ctx->pend_capture_id)) return QBA_OK;
+  return qba_fail(QBA_ESTATE, ctx->pend_captured
+                                  ? "a deferred reduction recorded inside a graph capture is still pending outside "
+                                    "it: call qba_flush_deferred before ending the capture"
+                                  : "a deferred reduction is pending from before a graph capture: call "
+                                    "qba_flush_deferred before beginning the capture");
+}
+
+// Only eager streams are ordered here: inside a capture the graph's own
+// dependencies order its nodes, and across a capture boundary the caller
+// synchronises (include/qba.h) -- an eager event cannot be waited on by a
+// capturing stream.  The capturing stream is tested first, so no other
+// stream is touched while one captures.
+int qba_slab_order(qba_ctx *ctx, hipStream_t stream) {
+  unsigned long long id = 0;
+  if (ctx->slab_used && ctx->slab_stream != stream && !qba_capture_of(stream, &id) &&
+      !qba_capture_of(ctx->slab_stream, &id)) {
+    if (!ctx->def_ev) QBA_HIP(hipEventCreateWithFlags(&ctx->def_ev, hipEventDisableTiming));
+    QBA_HIP(hipEventRecord(ctx->def_ev, ctx->slab_stream));
+    QBA_HIP(hipStreamWaitEvent(stream, ctx->def_ev, 0));
+  }
+  ctx->slab_stream = stream;
+  ctx->slab_used = true;
+  return QBA_OK;
+}
+
 int qba_flush_pending(qba_ctx *ctx, hipStream_t next) {
   auto &pd = ctx->pend;
   if (!pd.flush) return QBA_OK;
+  if (int rc = pend_capture_ok(ctx, pd.stream)) return rc;
+  if (next != pd.stream)
+    if (int rc = pend_capture_ok(ctx, next)) return rc;
   int (*f)(qba_ctx *) = pd.flush;
   int rc = f(ctx);
   pd.flush = nullptr;
@@ -165,6 +210,12 @@ extern "C" int qba_flush_deferred(qba_ctx *ctx) {
   if (!ctx->pend.flush) return QBA_OK;
   int rc = qba_set_device(ctx);
   if (rc) return rc;
+  if ((rc = pend_capture_ok(ctx, ctx->pend.stream))) {
+    // a captured reduction outside its capture cannot be launched any more:
+    // it is dropped (that call's counts stay incomplete) and the ctx is usable
+    if (ctx->pend_captured) ctx->pend.flush = nullptr;
+    return rc;
+  }
   return qba_flush_pending(ctx, ctx->pend.stream);
 }
 

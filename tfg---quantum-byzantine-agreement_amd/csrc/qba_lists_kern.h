@@ -1983,8 +1983,15 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     auto &pd = ctx->pend;
     int rc = QBA_OK;
     // a pending call of another n or on another stream is flushed on its own
+    // (qba_flush_pending refuses one recorded in another capture state)
     if (pd.flush && (pd.flush != &qba_flush_def<NP> || pd.stream != L.stream))
       if ((rc = qba_flush_pending(ctx, L.stream))) return rc;
+    unsigned long long cid = 0;
+    const int cap = qba_capture_of(L.stream, &cid);
+    if (pd.flush && (cap != ctx->pend_captured || (cap && cid != ctx->pend_capture_id)))
+      return qba_fail(QBA_ESTATE, "a deferred reduction is pending across a graph-capture boundary: call "
+                                  "qba_flush_deferred before beginning and before ending a capture");
+    if (!pd.flush && (rc = qba_slab_order(ctx, L.stream))) return rc;
     const size_t half_need = ((size_t)grid * C::NBP * sizeof(uint32_t) + 255) & ~(size_t)255;
     if (ctx->slab_bytes < 2 * half_need) {
       if ((rc = qba_flush_pending(ctx, L.stream))) return rc;
@@ -2010,10 +2017,16 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     pd.P = L.P;
     pd.stats = L.stats;
     pd.stream = L.stream;
+    ctx->pend_captured = cap;
+    ctx->pend_capture_id = cid;
+    ctx->slab_stream = L.stream;
+    ctx->slab_used = true;
     return QBA_OK;
   }
-  if (L.mode != 0)
+  if (L.mode != 0) {
     if (int rc = qba_flush_pending(ctx, L.stream)) return rc;
+    if (int rc = qba_slab_order(ctx, L.stream)) return rc;
+  }
   uint32_t *slab = nullptr;
   if (L.mode != 0) {
     int rc = qba_ensure_slab(ctx, (size_t)grid * C::NBP * sizeof(uint32_t));

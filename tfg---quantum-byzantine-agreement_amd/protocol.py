@@ -136,23 +136,28 @@ class PSet:
     # rank by several) arrives as the same wire array, so the order of the
     # last few distinct sequences is kept (keyed by the bytes, verified by
     # comparison; the arrays are never written in place)
+    # (one memo for the class: LocalWorld's thread scheduler runs ranks in
+    # threads, so lookups and evictions hold _memo_lock)
     _memo: Dict[tuple, tuple] = {}
+    _memo_lock = threading.Lock()
     _MEMO_MAX = 64
 
     @classmethod
     def build(cls, seq) -> "PSet":
         seq = np.ascontiguousarray(seq, dtype=np.int64)
         key = (len(seq), hash(seq.tobytes()))
-        hit = cls._memo.get(key)
+        with cls._memo_lock:
+            hit = cls._memo.get(key)
         if hit is not None and np.array_equal(hit[0], seq):
             return cls(hit[1])
         out = np.empty(max(len(seq), 1), np.int64)
         got = C.c_int64()
         call("qba_host_pyset_order", seq.ctypes.data, len(seq), out.ctypes.data, C.byref(got))
         order = out[:got.value]
-        if len(cls._memo) >= cls._MEMO_MAX:
-            cls._memo.pop(next(iter(cls._memo)))
-        cls._memo[key] = (seq.copy(), order)
+        with cls._memo_lock:
+            while len(cls._memo) >= cls._MEMO_MAX:
+                cls._memo.pop(next(iter(cls._memo)))
+            cls._memo[key] = (seq.copy(), order)
         return cls(order)
 
     def __len__(self) -> int:
@@ -320,7 +325,7 @@ class _Locked:
 class Party:
     """State of one rank: 0 = the QSD, 1 = commander, >= 2 = lieutenants."""
 
-    def __init__(self, comm, sizeL, nDishonest, engine, rng, log=None, lists=None, seed=0):
+    def __init__(self, comm, sizeL, nDishonest, engine, rng, log=None, lists=None, seed=0, wire=None):
         self.comm = comm
         self.rank = comm.Get_rank()
         self.n = comm.Get_size() - 1
@@ -343,6 +348,13 @@ class Party:
         self.wire = WireCache()
         self.tolerate_empty_vi = False  # run_local: record the reference's ValueError
         self.empty_vi_error = False
+        # In-process (LocalWorld) with a device engine, rank 0's list sends
+        # carry the device rows themselves (comm.DeviceRow, accounted as the
+        # wire messages): no lists -> int64-per-bit -> lists round trip.  The
+        # reference's wire codec stays for real MPI ranks and wire=True runs.
+        if wire is None:
+            wire = not (isinstance(comm, comm_mod.LocalComm) and hasattr(engine, "lists_to_bits"))
+        self.wire_lists = bool(wire)
 
     def say(self, *args):
         if self.log:
@@ -367,22 +379,40 @@ class Party:
         c, n, nq, sl = self.comm, self.n, self.nq, self.sizeL
         if self.rank == 0:
             self.say("|W| =", self.w)
-            raw = generacionListas(n, sl, nq, self.w, self.engine, self.seed, self.inject)
+            if self.wire_lists:
+                raw = generacionListas(n, sl, nq, self.w, self.engine, self.seed, self.inject)
+            else:  # the same messages, each carrying its device row (comm.DeviceRow)
+                dev = self._device_lists()
+                raw = [comm_mod.DeviceRow(dev[g, :sl], nq * sl) for g in range(n + 1)]
             reqs = [c.Isend([raw[0], _dt(c)], dest=1)]
             reqs += [c.Isend([raw[g], _dt(c)], dest=g) for g in range(1, n + 1)]
             for r in reqs:
                 r.Wait()
             return
-        mine = np.empty(nq * sl, np.int64)
+        buf = (lambda: np.empty(nq * sl, np.int64)) if self.wire_lists else (lambda: comm_mod.RowSlot(nq * sl))
+        mine = buf()
         req = c.Irecv([mine, _dt(c)], source=0)  # posted first: gets rawS[0] at rank 1
         if self.rank == 1:
-            extra = np.empty(nq * sl, np.int64)
+            extra = buf()
             c.Irecv([extra, _dt(c)], source=0).Wait()
             self.lc = self._decode(extra)
         req.Wait()
         self.li = self._decode(mine)
 
+    def _device_lists(self):
+        """generacionListas' lists (tfg.py:68-84) left on the device: sampled
+        (Philox keyed by entry, ``seed``) or the injected value array."""
+        n, sl = self.n, self.sizeL
+        if self.inject is None:
+            return self.engine.sample(n, self.seed, 0, sl)
+        arr = np.ascontiguousarray(self.inject, dtype=np.uint8)
+        if arr.shape != (n + 1, sl):
+            raise ValueError(f"injected lists must have shape {(n + 1, sl)}")
+        return self.engine.to_device(arr)
+
     def _decode(self, raw):
+        if isinstance(raw, comm_mod.RowSlot):  # in-process: the device row itself
+            return raw.row
         if hasattr(self.engine, "bits_to_values_host"):  # straight from the receive buffer
             return self.engine.bits_to_values_host(raw, self.sizeL, self.nq)
         return self.engine.bits_to_values(self.engine.to_device(raw), self.sizeL, self.nq)

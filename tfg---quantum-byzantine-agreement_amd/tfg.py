@@ -53,6 +53,9 @@ def _args(argv):
     ap.add_argument("--seed", type=int, default=None, help="rank RNG seed and list seed")
     ap.add_argument("--quiet", action="store_true", help="print only the outcome")
     ap.add_argument("--timing", action="store_true", help="print the wall time of the run")
+    ap.add_argument("--wire", action="store_true",
+                    help="in-process exact mode: send the lists in the reference's int64-per-bit wire layout "
+                         "(tfg.py:142-161) instead of handing each rank its device row")
     return ap.parse_args(argv)
 
 
@@ -149,7 +152,8 @@ def main(argv=None) -> int:
     party_cls = countmode.CountParty if a.mode == "count" else protocol.Party
     t0 = time.perf_counter()
     run = protocol.run_local(a.parties, size_l, a.nDishonest, eng, seed=seed, log=log,
-                             party_cls=party_cls, timeout=600, list_seed=list_seed)
+                             party_cls=party_cls, timeout=600, list_seed=list_seed,
+                             party_kwargs={"wire": True} if a.wire else None)
     _outcome(run.result, verbose)
     if a.timing:
         print(f"wall {time.perf_counter() - t0:.3f} s ({a.mode} mode, in-process, {a.parties + 1} ranks)")
