@@ -36,6 +36,18 @@
 #ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
 #define QBA_NT_STORE 1
 #endif
+#ifndef QBA_SAMP_TRIM  // closed sampler: rank fallback in its rare branch, no redundant mask / OR
+#define QBA_SAMP_TRIM 1
+#endif
+#ifndef QBA_SPLIT_LAST  // queue loop: all-active steps inlined without the activity mask
+#define QBA_SPLIT_LAST 1
+#endif
+#ifndef QBA_RANK_MASK  // not-Q entries read table entry 0 (LDS broadcast) instead of a random one
+#define QBA_RANK_MASK 1
+#endif
+#ifndef QBA_PUSH_W2  // pair-bin queue push as ds_write2_b32 (no register-pair move)
+#define QBA_PUSH_W2 0
+#endif
 
 
 template <int NP>
@@ -278,15 +290,31 @@ __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64
   // group g >= 1 = nibble g of (w1 low nibbles, w1 high nibbles, w0 high
   // nibbles) in byte order, group 0 = group 1: the masked words ARE the byte
   // layout, one v_perm in all (w0's low nibbles carry isQ and r)
+#if QBA_SAMP_TRIM
+  // unmasked: qba_closed_finish masks every not-Q word with ~qm & M4 anyway
+  c.nqr[0] = qba_perm_b(w1, w1, 0x03020101u);
+#else
   const uint32_t a = w1 & F::M4;
   c.nqr[0] = qba_perm_b(a, a, 0x03020101u);
+#endif
   c.nqr[1] = w1 >> 4;
   c.nqr[2] = w0 >> 4;
   c.nqr[3] = 0u;
   c.w0 = w0;
+#if QBA_SAMP_TRIM
+  // w1 is the rank word unless its Lemire test fails (P = (2^32 mod n!) /
+  // 2^32, 0.56 % at n = 11): the fallback words are chosen inside the rare
+  // branch, not by a select on every entry
+  uint32_t rank = w1;
+  if (__builtin_expect(!qba_accept<NP>(w1, F::T32), 0)) {
+    rank = w0 & ~31u;
+    if (!qba_accept<NP>(rank, F::T27)) {  // ~(T32 T27) / 2^59 per entry
+#else
   const bool o1 = qba_accept<NP>(w1, F::T32);
   uint32_t rank = o1 ? w1 : (w0 & ~31u);
   if (__builtin_expect(!o1 && !qba_accept<NP>(rank, F::T27), 0)) {  // ~(T32 T27) / 2^59 per entry
+  {
+#endif
     bool ok = false;
     for (uint32_t t = 1; !ok; ++t) {
       const QbaU4 y = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0x80000000u + t, h, k0, k1);
@@ -299,10 +327,13 @@ __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64
         }
     }
   }
+  }
   // a not-Q entry discards its table words (qba_closed_finish selects its
   // nibbles): rank 0 sends its three reads to one address per table, served
   // as an LDS broadcast, so only the Q lanes' random reads meet bank conflicts
+#if QBA_RANK_MASK
   rank &= (uint32_t)__builtin_amdgcn_sbfe((int)w0, 0, 1);
+#endif
   c.rank = rank;
 }
 
@@ -310,9 +341,16 @@ template <int NP>
 __device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint4 &A, const uint2 &sB,
                                                   uint32_t sC, uint32_t (&D)[CF<NP>::ND]) {
   using F = CF<NP>;
+#if QBA_SAMP_TRIM
+  // A.w (zero in the table) is kept alive by an empty asm, so the read stays
+  // one ds_read_b128 (4 LDS cycles, a ds_read_b96 takes 8) without an OR
+  uint32_t q[4] = {A.x, A.y, A.z, A.w};
+  asm volatile("" ::"v"(A.w));
+#else
   // A.w is zero in the table; folding it in keeps the read one ds_read_b128
   // (4 LDS cycles) instead of a ds_read_b96 (8).
   uint32_t q[4] = {A.x | A.w, A.y, A.z, A.w};
+#endif
   const uint32_t y0 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.x);
   uint32_t y1 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.y);
   if constexpr (F::RC > 1) y1 = qba_perm_b(y1, y0, sC);  // stage C moves window bytes 4..7 only
@@ -811,9 +849,12 @@ __device__ __forceinline__ void qba_count_pb(uint32_t c0, uint32_t c1, uint32_t 
   static_assert(NP == 11, "pair bins are laid out for n = 11");
   constexpr uint32_t B = QbaPB::BOFF * 4;
   const uint32_t E0 = (c0 << 2) & 0x3c3c3c3cu;  // groups 0-3, x4
-  const uint32_t E1 = (c0 >> 2) & 0x3c3c3c3cu;  // groups 4-7, x4
+  const uint32_t t = c0 >> 2;
+  const uint32_t E1 = t & 0x3c3c3c3cu;          // groups 4-7, x4
   const uint32_t E2 = c1 << 2;                  // groups 8-11, x4
-  const uint32_t hb = (__builtin_amdgcn_ubfe(c0, 8, 4) << 6) + hA;  // A + 64 u
+  // A + 64 u: u = group 1 sits at bits 6-9 of c0 >> 2, and A is 1-KiB
+  // aligned (qba_lists_body), so the base is one v_and_or
+  const uint32_t hb = (t & 0x3c0u) | hA;
   qba_lds_add(qba_add_word(hb, E0, 0) + B, 0x100u);      // group 0 at (x_0, u, u), B lanes 1-3
   qba_lds_add(qba_add_word(hb, E0, 1), 0x1u);            // (2,3)   A lane 0
   qba_lds_add(qba_add_word(hb, E1, 0), 0x100u);          // (4,5)   A lane 1
@@ -874,13 +915,21 @@ __device__ __forceinline__ void qba_q_push_pb(QbaWaveQ &q, const uint32_t (&D)[C
   const uint64_t m = __ballot(isq);
   const uint32_t mb = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
   if (isq) {
-    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     const uint32_t a = (((mb + q.tail + q.qn) << 3) & (uint32_t)(QBA_QCAP * 8 - 1)) | q.base;
     const uint2 c = qba_pb_pack<NP>(D);
+#if QBA_PUSH_W2
+    // ds_write2_b32: the two words from any VGPRs (a ds_write_b64 needs them
+    // as a pair: one v_mov per push).  LDS ops of a wave complete in order,
+    // so the drain's later read of the slot sees it, and the compiler's own
+    // lgkmcnt waits only over-count (never under-wait) for this asm.
+    asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(a), "v"(c.x), "v"(c.y) : "memory");
+#else
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     v2u cv;
     cv.x = c.x;
     cv.y = c.y;
     *reinterpret_cast<__attribute__((address_space(3))) v2u *>(static_cast<uintptr_t>(a)) = cv;
+#endif
   }
   q.qn += (uint32_t)__popcll(m);
   if (q.qn >= 64) qba_q_drain_pb<NP>(q, 64u);
@@ -1368,6 +1417,10 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   const uint64_t ts0 = wall_clock64();
 #endif
   uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
+  if constexpr (CNT) {  // pair bins: array A 1-KiB aligned (qba_count_pb ORs 64 u into its address)
+    const uint32_t h = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
+    hist += (((h + 1023u) & ~1023u) - h) / 4;
+  }
   if (MODE != 0) {
     constexpr int NZ = CNT ? QbaPB::AREA : C::NBP;
     for (int i = threadIdx.x; i < NZ; i += BS) hist[i] = 0u;
@@ -1403,6 +1456,15 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
     // wave-uniform trip count: pushes and drains always run with the whole wave
     for (uint32_t u = u0;; u += ustride) {
       const bool act = u < nunits;
+#if QBA_SPLIT_LAST
+      // every lane active (all steps but a wave's last): the step is inlined
+      // with act = true, so no per-pair activity mask is built (~1 VALU/entry)
+      if (__all(act)) {
+        qba_step_l<NP, MODE, SAMP, QPT, false, PK, true, CNT>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat,
+                                                              thr, pl, lists, ld, hist, &wq, true);
+        continue;
+      }
+#endif
       if (!__any(act)) break;
       qba_step_l<NP, MODE, SAMP, QPT, false, PK, true, CNT>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr,
                                                             pl, lists, ld, hist, &wq, act);
@@ -1881,7 +1943,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   // the fused closed-form kernel counts with pair bins (QbaPB)
   const bool pb = QbaUsePB<NP, 1, QBA_S_CLOSED>::value && L.mode == 1 && samp == QBA_S_CLOSED;
   if (pb) {
-    lds += (size_t)QbaPB::AREA * sizeof(uint32_t) + (size_t)(QBA_LBLOCK / 64 + 1) * QBA_QCAP * QbaPB::QSLOT;
+    lds += 1024 + (size_t)QbaPB::AREA * sizeof(uint32_t) + (size_t)(QBA_LBLOCK / 64 + 1) * QBA_QCAP * QbaPB::QSLOT;
   } else if (L.mode != 0) {
     lds += (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
     if (QBA_QUEUE) lds += (size_t)(QBA_LBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;

@@ -10,7 +10,7 @@ tag=${1:-ab}; shift || true
 out=$root/gpurun_out/$tag; mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 for r in $(seq 1 ${ROUNDS:-1}); do
-  for so in $root/tfg---quantum-byzantine-agreement_amd/_build/exp/*.so; do
+  for so in ${EXPDIR:-$root/tfg---quantum-byzantine-agreement_amd/_build/exp}/*.so; do
     name=$(basename $so .so)
     QBA_LIB=$so timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
         SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv \

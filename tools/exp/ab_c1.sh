@@ -6,13 +6,13 @@ root=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 out=$root/gpurun_out/${1:-ab_c1}; mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 for r in $(seq 1 ${ROUNDS:-2}); do
-  for so in $root/tfg---quantum-byzantine-agreement_amd/_build/exp/*.so; do
+  for so in ${EXPDIR:-$root/tfg---quantum-byzantine-agreement_amd/_build/exp}/*.so; do
     name=$(basename $so .so)
     QBA_LIB=$so timeout -k 10 120 python $root/bench.py --config 1 --steps 200 --warmup 50 --no-cpu-baseline > $out/$name.$r.json 2> $out/$name.$r.err
     python -c "import json; d=json.load(open('$out/$name.$r.json')); print('%-12s pass %d  %.2f us/step' % ('$name', $r, d['ms_per_step']*1e3))" | tee -a $out/summary.txt
   done
 done
-for so in $root/tfg---quantum-byzantine-agreement_amd/_build/exp/*.so; do
+for so in ${EXPDIR:-$root/tfg---quantum-byzantine-agreement_amd/_build/exp}/*.so; do
   name=$(basename $so .so)
   QBA_LIB=$so timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/$name.prof -o k -- \
      python $root/bench.py --config 1 --steps 200 --warmup 50 --no-cpu-baseline > $out/$name.prof.log 2>&1

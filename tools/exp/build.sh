@@ -8,7 +8,7 @@ here="$(cd "$(dirname "$0")/../../tfg---quantum-byzantine-agreement_amd/csrc" &&
 src=${SRC:-$here}
 name=$1; shift
 N=${N:-11}
-out=$here/../_build/exp; mkdir -p $out
+out=${EXPOUT:-$here/../_build/exp}; mkdir -p $out
 F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -fvisibility=hidden -munsafe-fp-atomics -I$here/../../include -DQBA_EXPERIMENT_BUILD"
 /opt/rocm/bin/hipcc $F -DQBA_ONLY_N=$N "$@" -c $src/qba_lists.hip -o $out/$name.o
 /opt/rocm/bin/hipcc $F -DQBA_INST_N=$N "$@" -c $src/qba_lists_inst.hip -o $out/${name}_n$N.o
