@@ -342,7 +342,7 @@ def headline(args):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u4 lists (nibble rows), i64 counts" if packed else "u8 lists (byte rows), i64 counts",
+        "dtype": _dtype(packed),
         "data": DATA,
         "config": {
             "workload": f"BASELINE configs[2] shard: n={n} parties, {args.dishonest} dishonest, "
@@ -386,6 +386,10 @@ def headline(args):
 # ---------------------------------------------------------------------------
 # the other configs (one GPU)
 # ---------------------------------------------------------------------------
+def _dtype(packed):
+    return "u4 lists (nibble rows), i64 counts" if packed else "u8 lists (byte rows), i64 counts"
+
+
 def _line(args, value, unit, workload, roofline, extra=None, higher=True, dtype="u8"):
     out = {"metric": METRIC, "value": value, "unit": unit, "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "higher_is_better": higher, "scaling": "weak", "vs_baseline": None,
@@ -498,7 +502,8 @@ def config1(args, eng):
                  {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": ach / HBM_PEAK_GBS, "traffic": None,
                   "note": ("6 MB of nibble-row" if packed else "12 MB of byte-row")
-                          + " lists stay in the 256 MB Infinity Cache; launch-bound"}, extra)
+                          + " lists stay in the 256 MB Infinity Cache; launch-bound"}, extra,
+                 dtype=_dtype(packed))
 
 
 def config3(args, eng, n_inst=4096, count=100_000):
@@ -531,7 +536,7 @@ def config3(args, eng, n_inst=4096, count=100_000):
                   "list_layout": "nibble rows (4 B/entry at n=7)" if packed else "byte rows (8 B/entry)",
                   "note": "BASELINE scores 2(n+1) = 16 B/entry (lists written + read back); the batched "
                           "kernel writes the lists once and never re-reads them, so frac can pass 1 -- "
-                          "written_gbs is the store stream it actually moves"}, extra)
+                          "written_gbs is the store stream it actually moves"}, extra, dtype=_dtype(packed))
 
 
 def config4(args, eng):

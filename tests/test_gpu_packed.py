@@ -235,3 +235,30 @@ def test_pairbin_no_recount_at_bench_size(engine):
         assert np.array_equal(a, b)
     del p
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_pairbin_kernel_small_launches_bit_exact(monkeypatch, packed):
+    """The pair-bin kernel (picked for launches of >= 2^24 entries) forced on
+    small and ragged launches with QBA_PB_MIN_ENTRIES=0: tails (partial quads,
+    counted entry by entry into the pair bins), odd first columns and a
+    chunked call, bit-exact against the C twin, no recount."""
+    monkeypatch.setenv("QBA_PB_MIN_ENTRIES", "0")
+    eng = sub("engine").Engine(0)
+    try:
+        n = 11
+        for first, count in [(0, 1), (0, 2), (3, 5), (0, 8), (1, 17), (10, 4099), (0, 100_003), (7, 2_000_001)]:
+            seed = 0xFACE + count
+            ref = _ref(eng, n, seed, first, count)
+            if packed:
+                p, c = eng.sample_check_packed(n, seed, first, count)
+                got = _unpack(p, count)
+            else:
+                lists, c = eng.sample_check(n, seed, first, count)
+                torch.cuda.synchronize()
+                got = lists[:, :count].cpu().numpy()
+            assert np.array_equal(got, ref), (first, count)
+            assert _same_counts(c, ref), (first, count)
+            assert list(eng.last_stats()) == [0, 0], (first, count)
+    finally:
+        eng.close()

@@ -47,6 +47,7 @@ extern "C" int qba_init(int device, qba_ctx **out) {
     const unsigned long long v = strtoull(c, nullptr, 10) & ~3ull;
     if (v >= 4 && v <= QBA_CHUNK) ctx->chunk = v;
   }
+  if (const char *c = getenv("QBA_PB_MIN_ENTRIES")) ctx->pb_min = strtoull(c, nullptr, 10);  // tests
   if (const char *c = getenv("QBA_LIST_GRID")) {  // tests: force many entries per workgroup
     const long v = strtol(c, nullptr, 10);
     if (v > 0 && v < (1l << 20)) ctx->list_grid = (int)v;

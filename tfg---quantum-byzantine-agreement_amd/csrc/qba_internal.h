@@ -26,7 +26,7 @@
     defined(QBA_WIDE_QPT) || defined(QBA_MINW) || defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) ||                \
     defined(QBA_RED_ALL_IN_FLIGHT) || defined(QBA_QUEUE) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) ||      \
     defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) ||               \
-    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N) || defined(QBA_PAIRBINS) || defined(QBA_SAMP_TRIM) || defined(QBA_SPLIT_LAST) || defined(QBA_RANK_MASK) || defined(QBA_PUSH_W2)
+    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N) || defined(QBA_PAIRBINS) || defined(QBA_SAMP_TRIM) || defined(QBA_SPLIT_LAST) || defined(QBA_RANK_MASK) || defined(QBA_PUSH_W2) || defined(QBA_PB_ALIGN) || defined(QBA_DEF_PAIRWISE)
 #ifndef QBA_EXPERIMENT_BUILD
 #error "an experiment switch is set without QBA_EXPERIMENT_BUILD (tools/exp/build.sh): not a shippable libqba"
 #endif
@@ -219,6 +219,7 @@ struct qba_ctx {
   void *rccl_comm = nullptr;
   int rccl_ranks = 0;
   int list_grid = 0;  // > 0: cap on the list kernels' workgroups, no per-workgroup budget (env QBA_LIST_GRID, tests)
+  uint64_t pb_min = 1ull << 24;  // entries from which the fused n = 11 kernel counts in pair bins (env QBA_PB_MIN_ENTRIES)
   // graph capture of the pending deferred reduction (pend): 1 when it was
   // recorded inside a capture, with that capture's id
   int pend_captured = 0;

@@ -33,6 +33,9 @@
 #ifndef QBA_PAIRWISE  // closed sampler: a quad's two pairs one after the other (fewer live VGPRs)
 #define QBA_PAIRWISE 1
 #endif
+#ifndef QBA_DEF_PAIRWISE  // ... in the deferred (configs[1]) kernel: interleaved, more ILP at low occupancy
+#define QBA_DEF_PAIRWISE 0
+#endif
 #ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
 #define QBA_NT_STORE 1
 #endif
@@ -40,7 +43,10 @@
 #define QBA_SAMP_TRIM 1
 #endif
 #ifndef QBA_SPLIT_LAST  // queue loop: all-active steps inlined without the activity mask
-#define QBA_SPLIT_LAST 1
+#define QBA_SPLIT_LAST 0    // (rejected: +4.4 VALU/entry, +5 % cycles, profiles/r4/ab_trim)
+#endif
+#ifndef QBA_PB_ALIGN  // pair bins: array A 1-KiB aligned, base = one v_and_or
+#define QBA_PB_ALIGN 1
 #endif
 #ifndef QBA_RANK_MASK  // not-Q entries read table entry 0 (LDS broadcast) instead of a random one
 #define QBA_RANK_MASK 1
@@ -593,7 +599,7 @@ __device__ __forceinline__ void qba_entry_d(uint64_t e, uint32_t k0, uint32_t k1
 }
 
 // Sample one quad (entries [c0, c0+4) of the launch) into the byte layout.
-template <int NP, int SAMP, bool TAIL>
+template <int NP, int SAMP, bool TAIL, int PW = QBA_PAIRWISE>
 __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t first, uint32_t k0,
                                                 uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                                 const uint64_t *pat, const uint64_t *apat,
@@ -601,8 +607,10 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
                                                 uint32_t (&D)[4][CF<NP>::ND]) {
   constexpr int ND = CF<NP>::ND;
   if constexpr (SAMP == QBA_S_CLOSED && !TAIL) {
-#if QBA_PAIRWISE  // each pair's table reads and finish before the next pair's Philox (fewer live VGPRs)
-    if (!(first & 1)) {
+    // PW: each pair's table reads and finish before the next pair's Philox
+    // (fewer live VGPRs: the 8-wave list kernel); else the quad's two Philox
+    // blocks interleaved (more ILP: the deferred kernel's low-occupancy step)
+    if (PW && !(first & 1)) {
       const uint32_t phi = (uint32_t)(first >> 33);
       const uint32_t plo = (uint32_t)(first >> 1) + (c0 >> 1);
 #pragma unroll
@@ -622,7 +630,6 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
       }
       return;
     }
-#endif
     if (!(first & 1)) {  // wave-uniform: the quad is two whole pairs
       QbaClosed cl[4];
       // A launch never crosses a multiple of 2^33 entries (dispatch splits
@@ -852,9 +859,13 @@ __device__ __forceinline__ void qba_count_pb(uint32_t c0, uint32_t c1, uint32_t 
   const uint32_t t = c0 >> 2;
   const uint32_t E1 = t & 0x3c3c3c3cu;          // groups 4-7, x4
   const uint32_t E2 = c1 << 2;                  // groups 8-11, x4
+#if QBA_PB_ALIGN
   // A + 64 u: u = group 1 sits at bits 6-9 of c0 >> 2, and A is 1-KiB
   // aligned (qba_lists_body), so the base is one v_and_or
   const uint32_t hb = (t & 0x3c0u) | hA;
+#else
+  const uint32_t hb = (__builtin_amdgcn_ubfe(c0, 8, 4) << 6) + hA;  // A + 64 u
+#endif
   qba_lds_add(qba_add_word(hb, E0, 0) + B, 0x100u);      // group 0 at (x_0, u, u), B lanes 1-3
   qba_lds_add(qba_add_word(hb, E0, 1), 0x1u);            // (2,3)   A lane 0
   qba_lds_add(qba_add_word(hb, E1, 0), 0x100u);          // (4,5)   A lane 1
@@ -960,7 +971,7 @@ __device__ __forceinline__ void qba_count_one(const uint32_t (&D)[CF<NP>::ND], u
 // 4*QPT-byte vector per thread (16 B at QPT = 4: a wave moves 1 KiB per row).
 // MODE 0: sample -> lists;  MODE 1: sample -> lists + counts;  MODE 2: lists -> counts
 // TAIL (QPT = 1 only): the last, partial quad, byte by byte.
-template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false, int CNT = 0>
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false, int CNT = 0, int PW = QBA_PAIRWISE>
 __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                          uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                          const uint64_t *pat, const uint64_t *apat,
@@ -1012,7 +1023,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
   } else {
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
-      qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
+      qba_sample_quad<NP, SAMP, TAIL, PW>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
 #pragma unroll
       for (int i = 0; i < ND; ++i)
         qba_t4(D[0][i], D[1][i], D[2][i], D[3][i], row[k][4 * i], row[k][4 * i + 1],
@@ -1098,7 +1109,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
 // QPT = 1 (unaligned starts, the tail quads): 2 bytes per row, stored as bytes
 // (a chunk may start at an odd byte).  MODE 2 reads the same layout; an
 // unpacked quad's entries come out permuted (counting is order-free).
-template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false, int CNT = 0>
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, bool WQ = false, int CNT = 0, int PW = QBA_PAIRWISE>
 __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                             uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                             const uint64_t *pat, const uint64_t *apat,
@@ -1160,7 +1171,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
     const uint32_t am = act ? 0xffu : 0u;
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
-      qba_sample_quad<NP, SAMP, TAIL>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
+      qba_sample_quad<NP, SAMP, TAIL, PW>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
         Dp[2 * k][i] = D[0][i] | (D[1][i] << 4);
@@ -1243,7 +1254,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
   }
 }
 
-template <int NP, int MODE, int SAMP, int QPT, bool TAIL, int PK, bool WQ = false, int CNT = 0>
+template <int NP, int MODE, int SAMP, int QPT, bool TAIL, int PK, bool WQ = false, int CNT = 0, int PW = QBA_PAIRWISE>
 __device__ __forceinline__ void qba_step_l(uint32_t c0, uint32_t count, uint64_t first, uint32_t k0,
                                            uint32_t k1, const QbaProgramSet *__restrict__ ps,
                                            const uint64_t *pat, const uint64_t *apat,
@@ -1251,9 +1262,9 @@ __device__ __forceinline__ void qba_step_l(uint32_t c0, uint32_t count, uint64_t
                                            uint8_t *__restrict__ lists, uint64_t ld, uint32_t *hist,
                                            QbaWaveQ *wq = nullptr, bool act = true) {
   if constexpr (PK)
-    qba_step_pk<NP, MODE, SAMP, QPT, TAIL, WQ, CNT>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
+    qba_step_pk<NP, MODE, SAMP, QPT, TAIL, WQ, CNT, PW>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
   else
-    qba_step<NP, MODE, SAMP, QPT, TAIL, WQ, CNT>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
+    qba_step<NP, MODE, SAMP, QPT, TAIL, WQ, CNT, PW>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist, wq, act);
 }
 
 // Stage the program's tables in LDS; returns the histogram base after them.
@@ -1344,9 +1355,16 @@ __device__ __forceinline__ bool qba_pb_flush(uint32_t *hist, uint32_t *row) {
     v[3] = s13 >> 16;      // (8,9)
     v[4] = sb;             // (10,11)
     g0 = Bw[xg + 16 * ug + 256 * ug] >> 8;
+    // lane totals: summed across the wave first (64 same-address LDS atomics
+    // per instruction serialise: +12 us per launch), then one atomic per wave
+    uint32_t s6[6] = {v[0], v[1], v[2], v[3], v[4], g0};
 #pragma unroll
-    for (int p = 0; p < 5; ++p) atomicAdd(&misc[p], v[p]);
-    atomicAdd(&misc[5], g0);
+    for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+      for (int p = 0; p < 6; ++p) s6[p] += __shfl_xor(s6[p], m, 64);
+    if ((t & 63) == 0)
+#pragma unroll
+      for (int p = 0; p < 6; ++p) atomicAdd(&misc[p], s6[p]);
   } else if (t < 512) {  // groups 3, 5, 7, 9, 11 (x_h of each pair): sums over x_g
     uint32_t s02 = 0u, s13 = 0u, sb = 0u;
     const uint4 *a = reinterpret_cast<const uint4 *>(A + 16 * ur + 256 * yr);
@@ -1402,7 +1420,7 @@ __device__ __forceinline__ bool qba_pb_flush(uint32_t *hist, uint32_t *row) {
 // PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row.
 // The body of the list kernel; its workgroups are those after the first
 // `red` (qba_k_lists: 0; qba_k_lists_def: its reduce workgroups).
-template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK, int CNT = 0>
+template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK, int CNT = 0, int PW = QBA_PAIRWISE>
 __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1,
                                                uint64_t first, uint32_t count, uint8_t *__restrict__ lists,
                                                uint64_t ld, uint32_t *__restrict__ slab, QbaZero zero,
@@ -1417,7 +1435,7 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   const uint64_t ts0 = wall_clock64();
 #endif
   uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
-  if constexpr (CNT) {  // pair bins: array A 1-KiB aligned (qba_count_pb ORs 64 u into its address)
+  if constexpr (CNT && QBA_PB_ALIGN) {  // pair bins: array A 1-KiB aligned (qba_count_pb ORs 64 u into its address)
     const uint32_t h = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     hist += (((h + 1023u) & ~1023u) - h) / 4;
   }
@@ -1460,13 +1478,13 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
       // every lane active (all steps but a wave's last): the step is inlined
       // with act = true, so no per-pair activity mask is built (~1 VALU/entry)
       if (__all(act)) {
-        qba_step_l<NP, MODE, SAMP, QPT, false, PK, true, CNT>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat,
+        qba_step_l<NP, MODE, SAMP, QPT, false, PK, true, CNT, PW>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat,
                                                               thr, pl, lists, ld, hist, &wq, true);
         continue;
       }
 #endif
       if (!__any(act)) break;
-      qba_step_l<NP, MODE, SAMP, QPT, false, PK, true, CNT>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr,
+      qba_step_l<NP, MODE, SAMP, QPT, false, PK, true, CNT, PW>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr,
                                                             pl, lists, ld, hist, &wq, act);
     }
     while (wq.qn) {  // wave-uniform
@@ -1477,17 +1495,17 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
     }
   } else {
     for (uint32_t u = u0; u < nunits; u += ustride)
-      qba_step_l<NP, MODE, SAMP, QPT, false, PK>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr, pl,
-                                           lists, ld, hist);
+      qba_step_l<NP, MODE, SAMP, QPT, false, PK, false, 0, PW>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat,
+                                                            thr, pl, lists, ld, hist);
   }
   // the remaining < 4 QPT entries: whole quads, then the partial one
   const uint32_t r0 = nunits * (4 * QPT), rq = (count - r0 + 3) >> 2;
   if (!(QBA_EXP_SKIP & 1) && bid == nblk - 1 && threadIdx.x < rq) {
     const uint32_t c0 = r0 + 4 * threadIdx.x;
     if (c0 + 4 <= count)
-      qba_step_l<NP, MODE, SAMP, 1, false, PK, false, CNT>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
+      qba_step_l<NP, MODE, SAMP, 1, false, PK, false, CNT, PW>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
     else
-      qba_step_l<NP, MODE, SAMP, 1, true, PK, false, CNT>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
+      qba_step_l<NP, MODE, SAMP, 1, true, PK, false, CNT, PW>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
   }
   if (MODE != 0) {
     __syncthreads();
@@ -1546,13 +1564,15 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   }
 }
 
-template <int NP, int MODE, int SAMP, int QPT, int PK>
+// CNT 1: pair-bin counting (QbaUsePB kernels only; the launcher picks it for
+// launches of at least ctx->pb_min entries).
+template <int NP, int MODE, int SAMP, int QPT, int PK, int CNT = 0>
 __global__ void QBA_LISTS_BOUNDS
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                 uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
                 uint32_t *__restrict__ slab, QbaZero zero) {
-  qba_lists_body<NP, MODE, SAMP, QPT, PK, QBA_LBLOCK, QbaUsePB<NP, MODE, SAMP>::value ? 1 : 0>(
-      ps, k0, k1, first, count, lists, ld, slab, zero, 0u);
+  static_assert(!CNT || QbaUsePB<NP, MODE, SAMP>::value, "pair bins: the fused closed-form n = 11 kernel only");
+  qba_lists_body<NP, MODE, SAMP, QPT, PK, QBA_LBLOCK, CNT>(ps, k0, k1, first, count, lists, ld, slab, zero, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -1687,8 +1707,8 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, QBA_DBLOCK),
                      reinterpret_cast<uint32_t *>(lds));
     return;
   }
-  qba_lists_body<NP, 1, SAMP, QPT, PK, QBA_DBLOCK>(ps, k0, k1, first, count, lists, ld, slab, zero,
-                                                   (uint32_t)d.red);
+  qba_lists_body<NP, 1, SAMP, QPT, PK, QBA_DBLOCK, 0, QBA_DEF_PAIRWISE>(ps, k0, k1, first, count, lists, ld, slab,
+                                                                     zero, (uint32_t)d.red);
 }
 
 // qba_flush_deferred: the last pending reduction on its own.
@@ -1940,8 +1960,12 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     if (int rc = check_closed<NP>(hs)) return rc;
     lds += table_lds<NP>(hs, samp);
   }
-  // the fused closed-form kernel counts with pair bins (QbaPB)
-  const bool pb = QbaUsePB<NP, 1, QBA_S_CLOSED>::value && L.mode == 1 && samp == QBA_S_CLOSED;
+  // the fused closed-form kernel counts with pair bins (QbaPB) when the
+  // launch is large enough to repay their flush (a fixed ~2 us per launch:
+  // 1e6 entries 17.7 vs 15.0 us, 1.25e8 entries 298 vs 313 us,
+  // profiles/r4/small_launch); QBA_LIST_GRID (tests) forces them
+  const bool pb = QbaUsePB<NP, 1, QBA_S_CLOSED>::value && L.mode == 1 && samp == QBA_S_CLOSED &&
+                  (L.count >= ctx->pb_min || ctx->list_grid > 0);
   if (pb) {
     lds += 1024 + (size_t)QbaPB::AREA * sizeof(uint32_t) + (size_t)(QBA_LBLOCK / 64 + 1) * QBA_QCAP * QbaPB::QSLOT;
   } else if (L.mode != 0) {
@@ -1973,9 +1997,15 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   if (L.mode == 2) {
     kern = QBA_K(2, QBA_S_GENERAL);
   } else if (samp == QBA_S_CLOSED) {
-    if constexpr (NP <= QBA_CLOSED_MAX_N)
+    if constexpr (NP <= QBA_CLOSED_MAX_N) {
       kern = L.mode == 0 ? QBA_K(0, QBA_S_CLOSED) : QBA_K(1, QBA_S_CLOSED);
-    else
+      if constexpr (QbaUsePB<NP, 1, QBA_S_CLOSED>::value)
+        if (pb)
+          kern = L.packed ? (wide ? (const void *)qba_k_lists<NP, 1, QBA_S_CLOSED, 2, 1, 1>
+                                  : (const void *)qba_k_lists<NP, 1, QBA_S_CLOSED, 1, 1, 1>)
+                          : (wide ? (const void *)qba_k_lists<NP, 1, QBA_S_CLOSED, QBA_WIDE_QPT, 0, 1>
+                                  : (const void *)qba_k_lists<NP, 1, QBA_S_CLOSED, 1, 0, 1>);
+    } else
       return qba_fail(QBA_EUNSUPPORTED, "closed form beyond n = 11");
   } else if (samp == QBA_S_FAST) {
     kern = L.mode == 0 ? QBA_K(0, QBA_S_FAST) : QBA_K(1, QBA_S_FAST);
