@@ -36,6 +36,12 @@
 #ifndef QBA_DEF_PAIRWISE  // ... in the deferred (configs[1]) kernel: interleaved, more ILP at low occupancy
 #define QBA_DEF_PAIRWISE 0
 #endif
+#ifndef QBA_DEF_GTAB  // deferred kernel: stage tables read from global memory, not staged in LDS
+#define QBA_DEF_GTAB 0
+#endif
+#ifndef QBA_DEF_WAVES  // deferred kernel: waves per SIMD it is compiled for
+#define QBA_DEF_WAVES 6
+#endif
 #ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
 #define QBA_NT_STORE 1
 #endif
@@ -1268,14 +1274,19 @@ __device__ __forceinline__ void qba_step_l(uint32_t c0, uint32_t count, uint64_t
 }
 
 // Stage the program's tables in LDS; returns the histogram base after them.
-template <int NP, int MODE, int SAMP, int BS>
+// GT: the closed-form stage tables are read from global memory (L1 / L2)
+// instead of being staged -- the deferred kernel's one-step workgroups
+// (configs[1]) spend longer staging 29 KB than their reads take.
+template <int NP, int MODE, int SAMP, int BS, int GT = 0>
 __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__ ps, uint64_t *lds,
                                                const uint64_t *&pat, const uint64_t *&apat,
                                                const uint64_t *&thr, const uint32_t *&pl) {
   pat = apat = thr = lds;
   pl = reinterpret_cast<const uint32_t *>(lds);
   uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
-  if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
+  if constexpr (GT && MODE != 2 && SAMP == QBA_S_CLOSED) {
+    pl = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
+  } else if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
     // 16-B loads, all issued before the first LDS write: one memory round
@@ -1420,7 +1431,8 @@ __device__ __forceinline__ bool qba_pb_flush(uint32_t *hist, uint32_t *row) {
 // PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row.
 // The body of the list kernel; its workgroups are those after the first
 // `red` (qba_k_lists: 0; qba_k_lists_def: its reduce workgroups).
-template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK, int CNT = 0, int PW = QBA_PAIRWISE>
+template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK, int CNT = 0, int PW = QBA_PAIRWISE,
+          int GT = 0>
 __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1,
                                                uint64_t first, uint32_t count, uint8_t *__restrict__ lists,
                                                uint64_t ld, uint32_t *__restrict__ slab, QbaZero zero,
@@ -1434,7 +1446,7 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   uint64_t *tsl = reinterpret_cast<uint64_t *>(slab + (size_t)nblk * C::NBP) + 8 * bid;
   const uint64_t ts0 = wall_clock64();
 #endif
-  uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
+  uint32_t *hist = qba_stage<NP, MODE, SAMP, BS, GT>(ps, lds, pat, apat, thr, pl);
   if constexpr (CNT && QBA_PB_ALIGN) {  // pair bins: array A 1-KiB aligned (qba_count_pb ORs 64 u into its address)
     const uint32_t h = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     hist += (((h + 1023u) & ~1023u) - h) / 4;
@@ -1696,7 +1708,7 @@ __device__ __forceinline__ void qba_reduce_u(const QbaDefer &d, int u, int part,
 // first d.red workgroups; the list workgroups follow (slab row = their index).
 template <int NP, int SAMP, int QPT, int PK>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, QBA_DBLOCK),
-                               amdgpu_waves_per_eu(SAMP == QBA_S_CLOSED ? 6 : 1)))
+                               amdgpu_waves_per_eu(SAMP == QBA_S_CLOSED ? QBA_DEF_WAVES : 1)))
     qba_k_lists_def(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                     uint32_t count, uint8_t *__restrict__ lists, uint64_t ld, uint32_t *__restrict__ slab,
                     QbaZero zero, QbaDefer d) {
@@ -1707,8 +1719,8 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, QBA_DBLOCK),
                      reinterpret_cast<uint32_t *>(lds));
     return;
   }
-  qba_lists_body<NP, 1, SAMP, QPT, PK, QBA_DBLOCK, 0, QBA_DEF_PAIRWISE>(ps, k0, k1, first, count, lists, ld, slab,
-                                                                     zero, (uint32_t)d.red);
+  qba_lists_body<NP, 1, SAMP, QPT, PK, QBA_DBLOCK, 0, QBA_DEF_PAIRWISE, QBA_DEF_GTAB>(ps, k0, k1, first, count, lists,
+                                                                                   ld, slab, zero, (uint32_t)d.red);
 }
 
 // qba_flush_deferred: the last pending reduction on its own.
@@ -2062,7 +2074,8 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   size_t dlds = 0;
   int dgrid = 0, dcap = 0;
   if (kd) {
-    dlds = table_lds<NP>(hs, samp) + (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
+    dlds = (QBA_DEF_GTAB && samp == QBA_S_CLOSED ? 0 : table_lds<NP>(hs, samp)) +
+           (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
     if (QBA_QUEUE) dlds += (size_t)(QBA_DBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
     const size_t rlds = (size_t)(QBA_DBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t);
     if (dlds < rlds) dlds = rlds;

@@ -26,7 +26,7 @@ for N in (1_000_000, 2_000_000, 4_000_000):
     E.sample_check(n, 1, 0, N, lists, counts)
     b.record()
     torch.cuda.synchronize()
-    grid = min(-(-(N // 4) // (2 * 768)), 512)
+    grid = min(-(-(N // 4) // (2 * 1024)), 512)  # qba_k_lists: QBA_LBLOCK threads, 2 quads each
     lib = ctypes.CDLL(os.environ["QBA_LIB"])
     buf = np.zeros(grid * 8, np.uint64)
     rc = lib.qba_exp_timing(E.ctx, n, grid, buf.ctypes.data_as(ctypes.c_void_p))
