@@ -225,21 +225,39 @@ def headline(args):
     packed = args.layout == "packed"
     lists = eng.alloc_packed(n, per) if packed else eng.alloc_lists(n, per)
     _, _, _, total = dist_mod.count_layout(n)
-    # N > 1: step i's count all-reduce runs asynchronously (RCCL's own stream)
-    # while step i+1 samples into the other count buffer; a buffer is reused
-    # only after its reduction has been waited for, and every reduction
-    # completes inside the timed region.
-    nbuf = 2 if world > 1 else 1
+    # The fused packed step defers its count reduction into the NEXT step's
+    # list kernel (qba_sample_check_packed_deferred: the pair-bin kernel runs
+    # the pending reduction in workgroups after its own, in the slots its
+    # early-finishing workgroups free), so step i's counts are complete once
+    # step i+1 is enqueued, and the last step's after the flush -- all inside
+    # the timed region.  N > 1: step i's all-reduce runs asynchronously (RCCL's
+    # own stream) as soon as its counts are complete; a count buffer is
+    # written again (by a later step's reduction) only after its all-reduce
+    # was waited for.
+    deferred = packed and args.mode == "fused" and os.environ.get("QBA_BENCH_DEFER", "1") == "1"
+    nbuf = 3 if world > 1 else 1
     flats = [torch.zeros(total, dtype=torch.int64, device=eng.device) for _ in range(nbuf)]
     counts = [eng_mod.Counts(*dist_mod.split_counts(f, n)) for f in flats]
     pending = [None] * nbuf
     stream = torch.cuda.current_stream()
 
-    def step(i):
-        b = i % nbuf
+    def wait_buf(b):
         if pending[b] is not None:
             pending[b].wait()
             pending[b] = None
+
+    def step(i):
+        b = i % nbuf
+        if deferred:
+            # this launch completes step i-1's counts (buffer (i-1) % nbuf)
+            # and later writes buffer b: both must be free of all-reduces
+            wait_buf((i - 1) % nbuf)
+            wait_buf(b)
+            eng.sample_check_packed(n, args.seed, first, per, lists, counts[b], deferred=True)
+            if i > 0 and world > 1:
+                pending[(i - 1) % nbuf] = dist_mod.allreduce_counts_async(flats[(i - 1) % nbuf])
+            return
+        wait_buf(b)
         if packed:
             if args.mode == "fused":
                 eng.sample_check_packed(n, args.seed, first, per, lists, counts[b])
@@ -257,15 +275,18 @@ def headline(args):
             eng.check_counts(lists, n, per, counts[b])
         pending[b] = dist_mod.allreduce_counts_async(flats[b])
 
-    def drain():
+    def drain(last):
+        if deferred and last >= 0:
+            eng.flush_deferred()  # the last step's reduction
+            if world > 1:
+                wait_buf(last % nbuf)
+                pending[last % nbuf] = dist_mod.allreduce_counts_async(flats[last % nbuf])
         for b in range(nbuf):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
+            wait_buf(b)
 
     for i in range(args.warmup):
         step(i)
-    drain()
+    drain(args.warmup - 1)
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -282,7 +303,7 @@ def headline(args):
         step(i)
         if per_step_events:
             ev[i][1].record(stream)
-    drain()
+    drain(args.steps - 1)
     if not per_step_events:
         ev[0][1].record(stream)
     torch.cuda.synchronize()
@@ -360,7 +381,8 @@ def headline(args):
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": f"qba_k_lists<{n},1,*> + qba_k_reduce" if args.mode == "fused"
+            "kernel": (f"qba_k_lists_pbdef<{n},*> (list kernel; the previous step's count reduction runs in "
+                       "its tail)" if deferred else f"qba_k_lists<{n},1,*> + qba_k_reduce") if args.mode == "fused"
                       else f"qba_k_lists<{n},0,*> + qba_k_lists<{n},2,*> + reduce",
             "algorithmic_bytes_per_entry": bytes_per_entry, "launch_ms": kern_ms,
             # the bytes the launch really moves (PMC) over the same time: the fused

@@ -171,10 +171,13 @@ QBA_API int qba_check_counts_packed(qba_ctx *ctx, int n_parties, const uint8_t *
  * 68-84, 182, 189, 291-294, 327, consistent() 87-98), but the call's H, C, P
  * and qba_last_stats are complete only after the NEXT deferred call on this
  * ctx or qba_flush_deferred(ctx): the next call's list kernel reduces this
- * call's slab rows in workgroups of its own (two alternating slab buffers).
- * A call whose list workgroups fill the chip, any non-deferred counting call
- * and qba_reserve flush the pending reduction first; a pending call on
- * another stream is flushed there and ordered by an event. */
+ * call's slab rows in workgroups of its own (two alternating slab buffers):
+ * ahead of its list workgroups for small calls, after them -- in the slots
+ * its early-finishing workgroups free -- for the pair-bin kernel of large n =
+ * 11 calls.  A small call whose list workgroups fill the chip, any
+ * non-deferred counting call and qba_reserve flush the pending reduction
+ * first; a pending call on another stream is flushed there and ordered by an
+ * event. */
 QBA_API int qba_sample_check_deferred(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
                                       uint64_t count, uint8_t *lists_dev, uint64_t ld, int64_t *H_dev,
                                       int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);

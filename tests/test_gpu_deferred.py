@@ -207,3 +207,47 @@ def test_deferred_capture_boundaries(engine):
     torch.cuda.synchronize()
     assert _eq(c2, _ref_counts(engine, n, 6, 0, count))
     assert list(engine.last_stats()) == [0, 0]
+
+
+def _stream_ref(engine, n, seed, first, count):
+    info = engine.prepare(n)
+    H, C, P, _ = oracle_lib.stream_counts(n, seed, first, count, info["notq"], info["q"], info["closed"])
+    return H, C, P
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_deferred_pairbin_tail_chain(engine, packed):
+    """Large deferred calls (>= 2^24 entries: the pair-bin kernel) run the
+    pending reduction in workgroups after their own (qba_k_lists_pbdef), and
+    small deferred calls reduce a pair-bin call's slab: a mixed chain, each
+    call into its own outputs, equal to the C twin."""
+    n = 11
+    calls = [(51, 7, 60_001), (52, 1000, 20_000_003), (53, 0, 17_000_000), (54, 5, 90_000), (55, 0, 16_777_216)]
+    outs = [_call(engine, packed, n, s, f, c) for s, f, c in calls]
+    engine.flush_deferred()
+    torch.cuda.synchronize()
+    for (s, f, c), o in zip(calls, outs):
+        assert _eq(o, _stream_ref(engine, n, s, f, c)), (s, f, c)
+    assert list(engine.last_stats()) == [0, 0]
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_deferred_pairbin_tail_forced_small(monkeypatch, packed):
+    """The tail-deferred pair-bin kernel forced on small, ragged calls
+    (QBA_PB_MIN_ENTRIES=0): a chain of deferred calls, one accumulating."""
+    monkeypatch.setenv("QBA_PB_MIN_ENTRIES", "0")
+    eng = sub("engine").Engine(0)
+    try:
+        n = 11
+        calls = [(61, 0, 1), (62, 3, 4099), (63, 10, 250_001), (64, 0, 1_000_000)]
+        outs = [_call(eng, packed, n, s, f, c) for s, f, c in calls]
+        acc = eng.alloc_counts(n)
+        for i, (f, c) in enumerate([(0, 30_001), (30_001, 70_000)]):
+            _call(eng, packed, n, 65, f, c, counts=acc, accumulate=i > 0)
+        eng.flush_deferred()
+        torch.cuda.synchronize()
+        for (s, f, c), o in zip(calls, outs):
+            assert _eq(o, _ref_counts(eng, n, s, f, c)), (s, f, c)
+        assert _eq(acc, _ref_counts(eng, n, 65, 0, 100_001))
+    finally:
+        eng.close()

@@ -1428,6 +1428,8 @@ __device__ __forceinline__ bool qba_pb_flush(uint32_t *hist, uint32_t *row) {
 #define QBA_LISTS_BOUNDS \
   __attribute__((amdgpu_flat_work_group_size(1, QBA_LBLOCK), amdgpu_waves_per_eu(SAMP == QBA_S_CLOSED ? 8 : 1)))
 #endif
+#define QBA_LISTS_BOUNDS_PB \
+  __attribute__((amdgpu_flat_work_group_size(1, QBA_LBLOCK), amdgpu_waves_per_eu(8)))
 // PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row.
 // The body of the list kernel; its workgroups are those after the first
 // `red` (qba_k_lists: 0; qba_k_lists_def: its reduce workgroups).
@@ -1436,10 +1438,13 @@ template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK, int 
 __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1,
                                                uint64_t first, uint32_t count, uint8_t *__restrict__ lists,
                                                uint64_t ld, uint32_t *__restrict__ slab, QbaZero zero,
-                                               uint32_t red) {
+                                               uint32_t red, uint32_t tail = 0) {
   using C = QCfg<NP>;
   extern __shared__ __align__(16) uint64_t lds[];
-  const uint32_t bid = blockIdx.x - red, nblk = gridDim.x - red;
+  // list workgroups: [red, gridDim.x - tail) (reduce workgroups of a
+  // deferred reduction ahead of them, qba_k_lists_def, or after them,
+  // qba_k_lists_pbdef)
+  const uint32_t bid = blockIdx.x - red, nblk = gridDim.x - red - tail;
   const uint64_t *pat, *apat, *thr;
   const uint32_t *pl;
 #ifdef QBA_EXP_TIMING  // experiment builds: per-workgroup phase timestamps after the slab rows
@@ -1730,6 +1735,28 @@ __global__ void __launch_bounds__(QBA_LBLOCK) qba_k_reduce_def(QbaDefer d) {
   constexpr int NP4 = qba_def_parts<NP>();
   qba_reduce_u<NP>(d, (int)blockIdx.x / NP4, (int)blockIdx.x % NP4, (int)threadIdx.x, QBA_LBLOCK,
                    reinterpret_cast<uint32_t *>(lds));
+}
+
+// The pair-bin kernel with a deferred reduction in its TAIL: the pending
+// call's reduce workgroups come after the list workgroups, so they are
+// dispatched as list workgroups finish -- into the slots of the ~20 % that
+// run one thread-step fewer (1.25e8 entries over 512 x 1024 threads is 29.8
+// steps) -- instead of a separate reduce launch after the list kernel.
+template <int NP, int QPT, int PK>
+__global__ void QBA_LISTS_BOUNDS_PB
+    qba_k_lists_pbdef(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
+                      uint32_t count, uint8_t *__restrict__ lists, uint64_t ld, uint32_t *__restrict__ slab,
+                      QbaZero zero, QbaDefer d) {
+  extern __shared__ __align__(16) uint64_t lds[];
+  const uint32_t nl = gridDim.x - (uint32_t)d.red;
+  if (blockIdx.x >= nl) {  // workgroup-uniform
+    constexpr int NP4 = qba_def_parts<NP>();
+    const int r = (int)(blockIdx.x - nl);
+    qba_reduce_u<NP>(d, r / NP4, r % NP4, (int)threadIdx.x, QBA_LBLOCK, reinterpret_cast<uint32_t *>(lds));
+    return;
+  }
+  qba_lists_body<NP, 1, QBA_S_CLOSED, QPT, PK, QBA_LBLOCK, 1>(ps, k0, k1, first, count, lists, ld, slab, zero, 0u,
+                                                              (uint32_t)d.red);
 }
 
 // Batched independent instances (BASELINE configs[3]): instance i is its own
@@ -2058,7 +2085,14 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   // slots together; otherwise the pending one is flushed and this call is
   // reduced at once (its results are then simply complete earlier).
   const void *kd = nullptr;
-  if (L.defer && L.mode == 1) {
+  // a large pair-bin launch defers into its own tail (qba_k_lists_pbdef)
+  const bool pbd = pb && L.defer && L.mode == 1;
+  if constexpr (QbaUsePB<NP, 1, QBA_S_CLOSED>::value)
+    if (pbd)
+      kd = L.packed ? (wide ? (const void *)qba_k_lists_pbdef<NP, 2, 1> : (const void *)qba_k_lists_pbdef<NP, 1, 1>)
+                    : (wide ? (const void *)qba_k_lists_pbdef<NP, QBA_WIDE_QPT, 0>
+                            : (const void *)qba_k_lists_pbdef<NP, 1, 0>);
+  if (!pbd && L.defer && L.mode == 1) {
 #define QBA_KD(S)                                                                                  \
   (L.packed ? (wide ? (const void *)qba_k_lists_def<NP, S, 2, 1> : (const void *)qba_k_lists_def<NP, S, 1, 1>) \
             : (wide ? (const void *)qba_k_lists_def<NP, S, QBA_WIDE_QPT, 0> : (const void *)qba_k_lists_def<NP, S, 1, 0>))
@@ -2073,7 +2107,13 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   // more, shorter workgroups; 9.6 vs 10.5 us per configs[1] pass)
   size_t dlds = 0;
   int dgrid = 0, dcap = 0;
-  if (kd) {
+  if (pbd) {  // the list kernel's own launch shape; its LDS covers a reduce workgroup's scratch
+    dlds = lds;
+    if (dlds < (size_t)(QBA_LBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t))
+      dlds = (size_t)(QBA_LBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t);
+    if (dlds > 65536) QBA_HIP(hipFuncSetAttribute(kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds));
+    dgrid = grid;
+  } else if (kd) {
     dlds = (QBA_DEF_GTAB && samp == QBA_S_CLOSED ? 0 : table_lds<NP>(hs, samp)) +
            (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
     if (QBA_QUEUE) dlds += (size_t)(QBA_DBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
@@ -2083,7 +2123,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     if (dlds > 65536) QBA_HIP(hipFuncSetAttribute(kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds));
     dgrid = grid_for(ctx, kd, dlds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1, &dcap, QBA_DBLOCK);
   }
-  if (kd && dgrid + qba_def_wgs<NP>() <= dcap) {
+  if (kd && (pbd || dgrid + qba_def_wgs<NP>() <= dcap)) {
     const int grid = dgrid;
     auto &pd = ctx->pend;
     int rc = QBA_OK;
@@ -2109,7 +2149,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     QbaDefer d{pd.slab, pd.rows, red, pd.acc, pd.sacc, pd.H, pd.C, pd.P, pd.stats};
     QbaZero zero{L.H, L.C, L.P, L.stats, 0u};  // the reduction writes every output word itself
     void *args[] = {&ps, (void *)&k0, (void *)&k1, &first, &count, &lists, &ld, &slab, &zero, &d};
-    QBA_HIP(hipLaunchKernel(kd, dim3(grid + red), dim3(QBA_DBLOCK), args, dlds, L.stream));
+    QBA_HIP(hipLaunchKernel(kd, dim3(grid + red), dim3(pbd ? QBA_LBLOCK : QBA_DBLOCK), args, dlds, L.stream));
     QBA_HIP(hipGetLastError());
     pd.flush = &qba_flush_def<NP>;
     pd.slab = slab;
