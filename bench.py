@@ -175,12 +175,21 @@ def verify_counts(n, seed, per, world, H, C, P):
     return out
 
 
+# Measured issue cost per wave64 VALU instruction on one SIMD at 8 waves
+# (tools/exp/valu_rate.hip, profiles/r4/micro/valu_rate.txt): simple ops
+# (v_add_u32 2.31, v_bitop3_b32 2.42) and the 64-bit multiply that
+# SQ_INSTS_VALU_INT64 counts (v_mad_u64_u32, 4.56 -- Philox's multiply)
+VALU_CYC_SIMPLE, VALU_CYC_INT64 = 2.31, 4.56
+
+
 def issue_roofline(tj, entries, launch_ms):
     """roofline.issue: the fused kernel's issue-side ceiling from the PMC
     counters of this build (tools/pmc_traffic.py: chip-wide medians per
     launch).  Shader cycles per launch = GRBM_GUI_ACTIVE / 8 (8 XCDs); a
-    wave64 VALU instruction issues in 2 cycles on a 32-lane CDNA4 SIMD, 1,024
-    SIMDs and 256 LDS units on the chip."""
+    wave64 VALU instruction issues in 2 cycles on a 32-lane CDNA4 SIMD at
+    best (valu_busy_frac), the 64-bit multiplies in ~4.6 (valu_busy_frac_weighted:
+    the measured costs above; v_perm_b32 / v_mul_*_u32 at 4.25 are priced as
+    simple ops, so it is still a floor); 1,024 SIMDs and 256 LDS units."""
     c = tj.get("issue_counters_per_launch") or {}
     if "GRBM_GUI_ACTIVE" not in c or "SQ_INSTS_VALU" not in c:
         return None
@@ -191,6 +200,10 @@ def issue_roofline(tj, entries, launch_ms):
            "valu_lane_ops_per_entry": c["SQ_INSTS_VALU"] * 64 / entries,
            "valu_insts_per_simd_cycle": valu_ipc,
            "valu_busy_frac": 2 * valu_ipc}
+    if "SQ_INSTS_VALU_INT64" in c:
+        i64 = c["SQ_INSTS_VALU_INT64"]
+        out["valu_busy_frac_weighted"] = ((c["SQ_INSTS_VALU"] - i64) * VALU_CYC_SIMPLE
+                                          + i64 * VALU_CYC_INT64) / (1024 * cyc)
     if "SQ_LDS_IDX_ACTIVE" in c:
         out["lds_active_frac"] = c["SQ_LDS_IDX_ACTIVE"] / (256 * cyc)
         out["lds_bank_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(c["SQ_LDS_IDX_ACTIVE"], 1.0)
@@ -198,11 +211,13 @@ def issue_roofline(tj, entries, launch_ms):
         out["lds_atomics_per_entry"] = c["SQ_INSTS_LDS_ATOMIC"] * 64 / entries
     if "SQ_INSTS_LDS" in c:
         out["lds_insts_per_entry"] = c["SQ_INSTS_LDS"] * 64 / entries
-    busy = {"VALU": out["valu_busy_frac"], "LDS": out.get("lds_active_frac", 0.0)}
+    busy = {"VALU": out.get("valu_busy_frac_weighted", out["valu_busy_frac"]),
+            "LDS": out.get("lds_active_frac", 0.0)}
     top = max(busy, key=busy.get)
     out["binds"] = (f"{top} issue ({busy[top]:.0%} busy; "
                     + ", ".join(f"{k} {v:.0%}" for k, v in busy.items() if k != top)
-                    + "): neither unit saturated, the rest is LDS / memory latency the 8 waves per SIMD do not hide")
+                    + ("): neither unit saturated, the rest is LDS / memory latency the 8 waves per SIMD do not hide"
+                       if busy[top] < 0.8 else "): saturated"))
     return out
 
 

@@ -18,7 +18,7 @@ __global__ __launch_bounds__(512) void k(uint32_t *out, uint32_t seed, uint64_t 
   const uint32_t c = 0xD2511F53u ^ seed;
   uint64_t cc;
   __syncthreads();
-  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int r = 0; r < REP; ++r) {
 #define MAD(m, a) asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(m), "=s"(cc) : "v"(a), "s"(c))  // carry-out SGPR pair reused, as the compiler does
 #define V2(op, a, b) asm volatile(op " %0, %0, %1" : "+v"(a) : "v"(b))
@@ -42,10 +42,14 @@ __global__ __launch_bounds__(512) void k(uint32_t *out, uint32_t seed, uint64_t 
       V3("v_perm_b32", a4, a0); V3("v_perm_b32", a5, a1); V3("v_perm_b32", a6, a2); V3("v_perm_b32", a7, a3);
     }
   }
-  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   const uint32_t x = (uint32_t)(m0 ^ m1 ^ m2 ^ m3 ^ m4 ^ m5 ^ m6 ^ m7) ^ a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
-  if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
+  if ((threadIdx.x & 63) == 0) {
+    const int w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    cyc[2 * w] = t1 - t0;      // shader cycles of this wave's loop
+    cyc[2 * w + 1] = r1 - r0;  // the same span in 100 MHz ticks
+  }
 }
 
 int main() {
@@ -54,8 +58,11 @@ int main() {
   uint32_t *out;
   uint64_t *cyc;
   (void)hipMalloc(&out, (size_t)1024 * 512 * 4);
-  (void)hipMalloc(&cyc, (size_t)1024 * 8 * 8);
-  static uint64_t h[1024 * 8];
+  (void)hipMalloc(&cyc, (size_t)1024 * 8 * 8 * 2);
+  static uint64_t h[1024 * 8 * 2];
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
   // (grid, block): 8 waves per SIMD (4 x 512 threads per CU), 1 wave per SIMD (1 x 256 per CU)
   const int cfg[2][2] = {{256 * 4, 512}, {256, 256}};
   for (int c = 0; c < 2; ++c) {
@@ -63,13 +70,21 @@ int main() {
     const double wps = nw / 1024.0;
     for (int o = 0; o < 6; ++o) {
       for (int it = 0; it < 2; ++it) hipLaunchKernelGGL(ks[o], dim3(grid), dim3(bs), 0, 0, out, 7u + it, cyc);
+      (void)hipEventRecord(e0, 0);
+      hipLaunchKernelGGL(ks[o], dim3(grid), dim3(bs), 0, 0, out, 9u, cyc);
+      (void)hipEventRecord(e1, 0);
       (void)hipDeviceSynchronize();
-      (void)hipMemcpy(h, cyc, nw * 8, hipMemcpyDeviceToHost);
-      double s = 0;
-      for (int i = 0; i < nw; ++i) s += (double)h[i];
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      (void)hipMemcpy(h, cyc, nw * 16, hipMemcpyDeviceToHost);
+      double s = 0, rt = 0;
+      for (int i = 0; i < nw; ++i) s += (double)h[2 * i], rt += (double)h[2 * i + 1];
+      const double ghz = s / (rt * 10.0);           // shader cycles per ns
       const double per_wave = s / nw / (8.0 * REP);  // shader cycles per instruction, one wave
-      printf("%-14s %6.2f cyc/inst per wave, %5.2f cyc/inst per SIMD (%.0f waves/SIMD)\n", names[o], per_wave,
-             per_wave / wps, wps);
+      // chip-level: the whole kernel's cycles (events x clock) over the wave-instructions each SIMD issued
+      const double simd = ms * 1e6 * ghz / (wps * 8.0 * REP);
+      printf("%-14s %6.2f cyc/inst per wave | kernel %.3f ms at %.2f GHz: %5.2f cyc/inst per SIMD (%.0f waves/SIMD)\n",
+             names[o], per_wave, ms, ghz, simd, wps);
     }
   }
   return hipGetLastError() != hipSuccess;
