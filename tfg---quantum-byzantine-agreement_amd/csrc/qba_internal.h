@@ -22,7 +22,7 @@
 // ---------------------------------------------------------------------------
 #if defined(QBA_EXP_LDSPAD) || defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||   \
     defined(QBA_EXP_CHEAPRNG) || defined(QBA_EXP_PADVALU) || defined(QBA_EXP_PADLDS) || defined(QBA_EXP_NOATOMIC) || \
-    defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_GRID) || defined(QBA_EXP_NARROW) ||          \
+    defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_GRID) ||          \
     defined(QBA_WIDE_QPT) || defined(QBA_MINW) || defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) ||                \
     defined(QBA_RED_ALL_IN_FLIGHT) || defined(QBA_QUEUE) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) ||      \
     defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) ||               \

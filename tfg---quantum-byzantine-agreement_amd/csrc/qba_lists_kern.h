@@ -36,9 +36,6 @@
 #ifndef QBA_DEF_PAIRWISE  // ... in the deferred (configs[1]) kernel: interleaved, more ILP at low occupancy
 #define QBA_DEF_PAIRWISE 0
 #endif
-#ifndef QBA_DEF_GTAB  // deferred kernel: stage tables read from global memory, not staged in LDS
-#define QBA_DEF_GTAB 0
-#endif
 #ifndef QBA_DEF_WAVES  // deferred kernel: waves per SIMD it is compiled for
 #define QBA_DEF_WAVES 6
 #endif
@@ -48,17 +45,11 @@
 #ifndef QBA_SAMP_TRIM  // closed sampler: rank fallback in its rare branch, no redundant mask / OR
 #define QBA_SAMP_TRIM 1
 #endif
-#ifndef QBA_SPLIT_LAST  // queue loop: all-active steps inlined without the activity mask
-#define QBA_SPLIT_LAST 0    // (rejected: +4.4 VALU/entry, +5 % cycles, profiles/r4/ab_trim)
-#endif
 #ifndef QBA_PB_ALIGN  // pair bins: array A 1-KiB aligned, base = one v_and_or
 #define QBA_PB_ALIGN 1
 #endif
 #ifndef QBA_RANK_MASK  // not-Q entries read table entry 0 (LDS broadcast) instead of a random one
 #define QBA_RANK_MASK 1
-#endif
-#ifndef QBA_PUSH_W2  // pair-bin queue push as ds_write2_b32 (no register-pair move)
-#define QBA_PUSH_W2 0
 #endif
 
 
@@ -934,19 +925,11 @@ __device__ __forceinline__ void qba_q_push_pb(QbaWaveQ &q, const uint32_t (&D)[C
   if (isq) {
     const uint32_t a = (((mb + q.tail + q.qn) << 3) & (uint32_t)(QBA_QCAP * 8 - 1)) | q.base;
     const uint2 c = qba_pb_pack<NP>(D);
-#if QBA_PUSH_W2
-    // ds_write2_b32: the two words from any VGPRs (a ds_write_b64 needs them
-    // as a pair: one v_mov per push).  LDS ops of a wave complete in order,
-    // so the drain's later read of the slot sees it, and the compiler's own
-    // lgkmcnt waits only over-count (never under-wait) for this asm.
-    asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(a), "v"(c.x), "v"(c.y) : "memory");
-#else
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     v2u cv;
     cv.x = c.x;
     cv.y = c.y;
     *reinterpret_cast<__attribute__((address_space(3))) v2u *>(static_cast<uintptr_t>(a)) = cv;
-#endif
   }
   q.qn += (uint32_t)__popcll(m);
   if (q.qn >= 64) qba_q_drain_pb<NP>(q, 64u);
@@ -1274,19 +1257,14 @@ __device__ __forceinline__ void qba_step_l(uint32_t c0, uint32_t count, uint64_t
 }
 
 // Stage the program's tables in LDS; returns the histogram base after them.
-// GT: the closed-form stage tables are read from global memory (L1 / L2)
-// instead of being staged -- the deferred kernel's one-step workgroups
-// (configs[1]) spend longer staging 29 KB than their reads take.
-template <int NP, int MODE, int SAMP, int BS, int GT = 0>
+template <int NP, int MODE, int SAMP, int BS>
 __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__ ps, uint64_t *lds,
                                                const uint64_t *&pat, const uint64_t *&apat,
                                                const uint64_t *&thr, const uint32_t *&pl) {
   pat = apat = thr = lds;
   pl = reinterpret_cast<const uint32_t *>(lds);
   uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
-  if constexpr (GT && MODE != 2 && SAMP == QBA_S_CLOSED) {
-    pl = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
-  } else if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
+  if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
     // 16-B loads, all issued before the first LDS write: one memory round
@@ -1433,8 +1411,7 @@ __device__ __forceinline__ bool qba_pb_flush(uint32_t *hist, uint32_t *row) {
 // PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row.
 // The body of the list kernel; its workgroups are those after the first
 // `red` (qba_k_lists: 0; qba_k_lists_def: its reduce workgroups).
-template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK, int CNT = 0, int PW = QBA_PAIRWISE,
-          int GT = 0>
+template <int NP, int MODE, int SAMP, int QPT, int PK, int BS = QBA_LBLOCK, int CNT = 0, int PW = QBA_PAIRWISE>
 __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1,
                                                uint64_t first, uint32_t count, uint8_t *__restrict__ lists,
                                                uint64_t ld, uint32_t *__restrict__ slab, QbaZero zero,
@@ -1451,7 +1428,7 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   uint64_t *tsl = reinterpret_cast<uint64_t *>(slab + (size_t)nblk * C::NBP) + 8 * bid;
   const uint64_t ts0 = wall_clock64();
 #endif
-  uint32_t *hist = qba_stage<NP, MODE, SAMP, BS, GT>(ps, lds, pat, apat, thr, pl);
+  uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
   if constexpr (CNT && QBA_PB_ALIGN) {  // pair bins: array A 1-KiB aligned (qba_count_pb ORs 64 u into its address)
     const uint32_t h = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     hist += (((h + 1023u) & ~1023u) - h) / 4;
@@ -1491,15 +1468,6 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
     // wave-uniform trip count: pushes and drains always run with the whole wave
     for (uint32_t u = u0;; u += ustride) {
       const bool act = u < nunits;
-#if QBA_SPLIT_LAST
-      // every lane active (all steps but a wave's last): the step is inlined
-      // with act = true, so no per-pair activity mask is built (~1 VALU/entry)
-      if (__all(act)) {
-        qba_step_l<NP, MODE, SAMP, QPT, false, PK, true, CNT, PW>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat,
-                                                              thr, pl, lists, ld, hist, &wq, true);
-        continue;
-      }
-#endif
       if (!__any(act)) break;
       qba_step_l<NP, MODE, SAMP, QPT, false, PK, true, CNT, PW>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr,
                                                             pl, lists, ld, hist, &wq, act);
@@ -1724,7 +1692,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, QBA_DBLOCK),
                      reinterpret_cast<uint32_t *>(lds));
     return;
   }
-  qba_lists_body<NP, 1, SAMP, QPT, PK, QBA_DBLOCK, 0, QBA_DEF_PAIRWISE, QBA_DEF_GTAB>(ps, k0, k1, first, count, lists,
+  qba_lists_body<NP, 1, SAMP, QPT, PK, QBA_DBLOCK, 0, QBA_DEF_PAIRWISE>(ps, k0, k1, first, count, lists,
                                                                                    ld, slab, zero, (uint32_t)d.red);
 }
 
@@ -2017,18 +1985,14 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   lds = (lds + 15) & ~(size_t)15;
   if (lds == 0) lds = 16;
   // 4*QPT-byte row vectors (QPT quads per thread-step) when the rows allow it
-#ifdef QBA_EXP_NARROW
-  const bool wide = false;
-#else
   constexpr uintptr_t VA = 4 * QBA_WIDE_QPT - 1;  // row vectors need their natural alignment
   // (the one-quad step on twice the workgroups for small launches shortens
   // the list kernel -- 8.8 vs 10.1 us at 1e6 entries -- but its workgroups
   // then share CUs with the deferred reduction's: 11.7 vs 10.3 us per
-  // configs[1] step, profiles/r3/r3m, r3n; not taken, tools/exp/rejected)
+  // configs[1] step, profiles/r3/r3m, r3n; rejected, tools/exp/rejected)
   // nibble rows: the wide step stores one 4-B word per row (QPT = 2)
   const uintptr_t va = L.packed ? 3 : VA;
   const bool wide = !(reinterpret_cast<uintptr_t>(L.lists) & va) && !(L.ld & va);
-#endif
 #define QBA_K(M, S)                                                                          \
   (L.packed ? (wide ? (const void *)qba_k_lists<NP, M, S, 2, 1> : (const void *)qba_k_lists<NP, M, S, 1, 1>) \
             : (wide ? (const void *)qba_k_lists<NP, M, S, QBA_WIDE_QPT, 0> : (const void *)qba_k_lists<NP, M, S, 1, 0>))
@@ -2114,7 +2078,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     if (dlds > 65536) QBA_HIP(hipFuncSetAttribute(kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds));
     dgrid = grid;
   } else if (kd) {
-    dlds = (QBA_DEF_GTAB && samp == QBA_S_CLOSED ? 0 : table_lds<NP>(hs, samp)) +
+    dlds = table_lds<NP>(hs, samp) +
            (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
     if (QBA_QUEUE) dlds += (size_t)(QBA_DBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
     const size_t rlds = (size_t)(QBA_DBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t);
