@@ -48,6 +48,9 @@
 #ifndef QBA_PB_ALIGN  // pair bins: array A 1-KiB aligned, base = one v_and_or
 #define QBA_PB_ALIGN 1
 #endif
+#ifndef QBA_PB_CHECK_DISTINCT  // pair bins: per-entry distinctness test + equal-pair slow path (experiment)
+#define QBA_PB_CHECK_DISTINCT 0
+#endif
 #ifndef QBA_RANK_MASK  // not-Q entries read table entry 0 (LDS broadcast) instead of a random one
 #define QBA_RANK_MASK 1
 #endif
@@ -488,9 +491,12 @@ __device__ __forceinline__ uint32_t qba_byte_of(int g, uint32_t w0, uint32_t w1,
 //   Q-correlated iff L0 != L1 (tfg.py:327); u = L1 (tfg.py:182);
 //   H[u][g][L_g] += 1 for every g; C[u][g][h] += 1 for every equal pair --
 //   the pair loop runs only when the entry's distinct-value count (union of
-//   16-bit one-hots) is below n+1.
+//   16-bit one-hots) is below n+1.  DIST: the entry comes from the closed-form
+//   sampler, whose Q entries hold n+1 distinct values by construction (the
+//   stage tables are permutations, checked by qba_plan): no C bin can count,
+//   so the test is skipped (see qba_count_pb).
 // ---------------------------------------------------------------------------
-template <int NP>
+template <int NP, bool DIST = false>
 __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uint32_t one,
                                             uint32_t *hist, bool in_range, bool known_q = false,
                                             uint32_t hoff = 0xffffffffu) {
@@ -544,6 +550,7 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
 #ifdef QBA_EXP_NOSEEN
   return;
 #endif
+  if constexpr (DIST && !QBA_PB_CHECK_DISTINCT) return;
   uint32_t U = 0;
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) {
@@ -744,7 +751,7 @@ __device__ __forceinline__ uint32_t qba_queue_base(uint32_t *hist) {
 // Count the nv (<= 64) oldest queued entries, one per lane.  TRUSTED: the
 // values were produced by this kernel's sampler, masked to nq bits, so
 // Cond2's range test cannot fail and is skipped (check-only launches keep it).
-template <int NP, bool TRUSTED>
+template <int NP, bool TRUSTED, bool DIST = false>
 __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_t nv) {
   constexpr int ND = CF<NP>::ND;
   const uint32_t lane = __lane_id();
@@ -757,7 +764,7 @@ __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_
   __builtin_amdgcn_s_setprio(2);
 #pragma unroll
   for (int i = 0; i < ND; ++i) D[i] = *qba_lds(a + i * QBA_QCAP * 4);
-  if (nv >= 64 || lane < nv) qba_count_d<NP>(D, 0x00010001u, hist, TRUSTED, true, q.hoff);
+  if (nv >= 64 || lane < nv) qba_count_d<NP, DIST>(D, 0x00010001u, hist, TRUSTED, true, q.hoff);
   __builtin_amdgcn_s_setprio(0);
   q.tail += nv;
   q.qn -= nv;
@@ -766,7 +773,7 @@ __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_
 // Append the lanes' entries with isq set (in lane order) and count a full
 // batch of 64 as soon as one is queued.  Slot = tail + qn + the number of
 // queued lanes below this one (mbcnt adds the base for free).
-template <int NP, bool TRUSTED>
+template <int NP, bool TRUSTED, bool DIST = false>
 __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], bool isq,
                                            uint32_t *hist) {
   constexpr int ND = CF<NP>::ND;
@@ -780,7 +787,7 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
     for (int i = 0; i < ND; ++i) *qba_lds(a + i * QBA_QCAP * 4) = D[i];
   }
   q.qn += (uint32_t)__popcll(m);
-  if (q.qn >= 64) qba_q_drain<NP, TRUSTED>(q, hist, 64u);
+  if (q.qn >= 64) qba_q_drain<NP, TRUSTED, DIST>(q, hist, 64u);
 }
 
 // ---------------------------------------------------------------------------
@@ -869,7 +876,13 @@ __device__ __forceinline__ void qba_count_pb(uint32_t c0, uint32_t c1, uint32_t 
   qba_lds_add(qba_add_word(hb, E1, 1), 0x10000u);        // (6,7)   A lane 2
   qba_lds_add(qba_add_word(hb, E2, 0), 0x1000000u);      // (8,9)   A lane 3
   qba_lds_add(qba_add_word(hb, E2, 1) + B, 0x1u);        // (10,11) B lane 0
-  // distinctness (Cond 3 fast path): union of the 12 one-hots, 2 per op
+#if QBA_PB_CHECK_DISTINCT
+  // distinctness (Cond 3 fast path): union of the 12 one-hots, 2 per op.
+  // Not needed in the shipped build: pair bins count only the closed-form
+  // sampler's own entries (QbaUsePB), whose 12 values r ^ pi(g) are distinct
+  // for every Q entry because the stage tables are permutations -- which
+  // qba_plan checks when it builds them (check_perm_tables) -- so every C bin
+  // stays 0 without this test (-12 VALU per Q entry).
   const uint32_t one = 0x00010001u;
   uint32_t U = qba_pk_onehot(c0, one) | qba_pk_onehot(c0 >> 4, one) | qba_pk_onehot(c0 >> 8, one);
   U |= qba_pk_onehot(c0 >> 12, one) | qba_pk_onehot(c1, one) | qba_pk_onehot(c1 >> 8, one);
@@ -892,6 +905,7 @@ __device__ __forceinline__ void qba_count_pb(uint32_t c0, uint32_t c1, uint32_t 
           qba_lds_add(hA + B + 4 * (uint32_t)((k & 15) + 16 * u + 256 * (u ^ (1 + (k >> 4)))), 0x100u);
     }
   }
+#endif
 }
 
 // the queue's 8-B form of an entry in the byte layout (values < 16)
@@ -937,21 +951,21 @@ __device__ __forceinline__ void qba_q_push_pb(QbaWaveQ &q, const uint32_t (&D)[C
 
 // Push (the wave queue) / count one entry directly (tails) with the counting
 // scheme CNT (0: classic 32-bit bins in `hist`, 1: pair bins, hist = array A).
-template <int NP, bool TRUSTED, int CNT>
+template <int NP, bool TRUSTED, int CNT, bool DIST = false>
 __device__ __forceinline__ void qba_push(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], bool isq, uint32_t *hist) {
   if constexpr (CNT == 1)
     qba_q_push_pb<NP>(q, D, isq);
   else
-    qba_q_push<NP, TRUSTED>(q, D, isq, hist);
+    qba_q_push<NP, TRUSTED, DIST>(q, D, isq, hist);
 }
-template <int NP, int CNT>
+template <int NP, int CNT, bool DIST = false>
 __device__ __forceinline__ void qba_count_one(const uint32_t (&D)[CF<NP>::ND], uint32_t *hist) {
   if constexpr (CNT == 1) {
     if ((D[0] & 0xffu) == ((D[0] >> 8) & 0xffu)) return;  // not Q-correlated (tfg.py:327)
     const uint2 c = qba_pb_pack<NP>(D);
     qba_count_pb<NP>(c.x, c.y, (uint32_t)(uintptr_t)(qba_lds_u32 *)hist);
   } else {
-    qba_count_d<NP>(D, 0x00010001u, hist, true);
+    qba_count_d<NP, DIST>(D, 0x00010001u, hist, true);
   }
 }
 
@@ -1023,7 +1037,8 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
           // row 0 XOR row 1 is nonzero iff entry j is Q-correlated
           const uint32_t xq = (row[k][0] ^ row[k][1]) & (act ? 0xffffffffu : 0u);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) qba_push<NP, MODE == 1, CNT>(*wq, D[j], (xq & (0xffu << (8 * j))) != 0u, hist);
+          for (int j = 0; j < 4; ++j)
+            qba_push<NP, MODE == 1, CNT, SAMP == QBA_S_CLOSED>(*wq, D[j], (xq & (0xffu << (8 * j))) != 0u, hist);
         } else if constexpr (CNT == 1) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -1174,13 +1189,13 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
           for (int p = 0; p < 2; ++p) {
             const uint32_t w0 = Dp[2 * k + p][0];
             const uint32_t x = (w0 ^ (w0 >> 8)) & am;
-            qba_push<NP, true, CNT>(*wq, D[2 * p], (x & 0x0fu) != 0u, hist);
-            qba_push<NP, true, CNT>(*wq, D[2 * p + 1], x > 0x0fu, hist);
+            qba_push<NP, true, CNT, SAMP == QBA_S_CLOSED>(*wq, D[2 * p], (x & 0x0fu) != 0u, hist);
+            qba_push<NP, true, CNT, SAMP == QBA_S_CLOSED>(*wq, D[2 * p + 1], x > 0x0fu, hist);
           }
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (j < valid) qba_count_one<NP, CNT>(D[j], hist);
+            if (j < valid) qba_count_one<NP, CNT, SAMP == QBA_S_CLOSED>(D[j], hist);
         }
       }
     }
@@ -1476,7 +1491,7 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
       if constexpr (CNT)
         qba_q_drain_pb<NP>(wq, wq.qn < 64 ? wq.qn : 64u);
       else
-        qba_q_drain<NP, MODE == 1>(wq, hist, wq.qn < 64 ? wq.qn : 64u);
+        qba_q_drain<NP, MODE == 1, MODE == 1 && SAMP == QBA_S_CLOSED>(wq, hist, wq.qn < 64 ? wq.qn : 64u);
     }
   } else {
     for (uint32_t u = u0; u < nunits; u += ustride)
@@ -1763,7 +1778,7 @@ __global__ void __launch_bounds__(QBA_BLOCK)
       qba_step_l<NP, 1, SAMP, QPT, false, PK, true>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl,
                                               L, ld, hist, &wq, act);
     }
-    while (wq.qn) qba_q_drain<NP, true>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
+    while (wq.qn) qba_q_drain<NP, true, SAMP == QBA_S_CLOSED>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
 #else
     for (uint32_t u = threadIdx.x; u < nunits; u += QBA_BLOCK)
       qba_step_l<NP, 1, SAMP, QPT, false, PK>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,

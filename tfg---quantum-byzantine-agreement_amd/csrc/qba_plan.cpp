@@ -183,6 +183,47 @@ static void build_perm_tables(int n, std::vector<uint32_t> &words, uint32_t &ra,
   stage(radC, (int)radB.size(), true);
 }
 
+// What the fused pair-bin counter relies on (qba_lists_kern.h, qba_count_pb):
+// every Q entry the closed sampler draws holds n+1 DISTINCT values r ^ pi(g).
+// That holds when each stage-A row's bytes 0..n are a permutation of 0..n and
+// each B / C selector permutes the window while fixing its bytes past n (the
+// zero padding).  Checked once per program build; a violation is an error.
+static bool check_perm_tables(int n, const std::vector<uint32_t> &w, uint32_t ra, uint32_t rb, uint32_t rc,
+                              int offB, int offC) {
+  const int base = n >= 8 ? 4 : 0;
+  auto byte = [&](size_t word, int b) { return (int)((w[word] >> (8 * b)) & 0xffu); };
+  for (uint32_t i = 0; i < ra; ++i) {
+    uint32_t seen = 0;
+    for (int b = 0; b <= n; ++b) {
+      const int v = byte(4 * (size_t)i + b / 4, b % 4);
+      if (v > n || (seen >> v & 1u)) return false;
+      seen |= 1u << v;
+    }
+  }
+  // a selector over window bytes [lo, hi]: a permutation of them fixing every byte past n
+  auto perm_ok = [&](const int *sel, int lo, int hi) {
+    uint32_t seen = 0;
+    for (int b = lo; b <= hi; ++b) {
+      const int v = sel[b - lo];
+      if (v < lo || v > hi || (seen >> v & 1u)) return false;
+      if (base + b > n && v != b) return false;
+      seen |= 1u << v;
+    }
+    return true;
+  };
+  for (uint32_t i = 0; i < rb; ++i) {
+    int sel[8];
+    for (int b = 0; b < 8; ++b) sel[b] = byte((size_t)offB + 2 * i + b / 4, b % 4);
+    if (!perm_ok(sel, 0, 7)) return false;
+  }
+  for (uint32_t i = 0; i < rc && rc > 1; ++i) {
+    int sel[4];
+    for (int b = 0; b < 4; ++b) sel[b] = byte((size_t)offC + i, b);
+    if (!perm_ok(sel, 4, 7)) return false;
+  }
+  return true;
+}
+
 int qba_plan_gates(int n, int kind, const int32_t *gates, int ngates, const int32_t *perm,
                    std::vector<int32_t> &kept) {
   const int nq = qba_nq(n), N = (n + 1) * nq;
@@ -324,7 +365,11 @@ int qba_plan_image(int n, const QbaHostProgram &a, const QbaHostProgram &b, std:
   std::vector<uint32_t> pw;
   uint32_t ra = 1, rb = 1, rc = 1;
   int offB = 0, offC = 0;
-  if (closed) build_perm_tables(n, pw, ra, rb, rc, offB, offC);
+  if (closed) {
+    build_perm_tables(n, pw, ra, rb, rc, offB, offC);
+    if (!check_perm_tables(n, pw, ra, rb, rc, offB, offC))
+      return qba_fail(QBA_EINVAL, "closed-form stage tables are not permutations (internal error)");
+  }
   if (pw.size() > QBA_PERM_MAX_WORDS) return qba_fail(QBA_EINVAL, "permutation tables too large");
   // stage tables 16-B aligned and padded to whole 16-B words: the list kernels
   // stage them into LDS with 16-B loads
