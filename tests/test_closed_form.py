@@ -72,6 +72,33 @@ def test_stage_tables_compose_to_fisher_yates(n):
         assert compose(n, sizes, words, int(R)) == fy_decode(n, int(R)), (n, R)
 
 
+@pytest.mark.parametrize("n", list(range(1, 12)))
+def test_stage_tables_are_permutations(n):
+    """What the fused kernels rely on when they skip the per-entry equal-pair
+    test (qba_count_pb / qba_count_d with DIST): every
+    stage-A row holds 0..n once, every B selector permutes the 8 window bytes
+    and every C hi selector the window's bytes 4..7, each fixing the bytes
+    past n -- so each Q entry's values r ^ pi(g) are distinct.  qba_plan checks
+    the same when it builds a program (check_perm_tables); this pins it on
+    the exported tables."""
+    sizes, words = tables(n)
+    ra, rb, rc, offb, offc, _ = (int(x) for x in sizes)
+    base = 4 if n >= 8 else 0
+    b = lambda w, k: (int(w) >> (8 * k)) & 0xFF  # noqa: E731
+    for i in range(ra):
+        row = [b(words[4 * i + g // 4], g % 4) for g in range(n + 1)]
+        assert sorted(row) == list(range(n + 1)), (n, i, row)
+
+    def perm_ok(sel, lo, hi):
+        assert sorted(sel) == list(range(lo, hi + 1)), sel
+        assert all(sel[k - lo] == k for k in range(lo, hi + 1) if base + k > n), sel
+
+    for i in range(rb):
+        perm_ok([b(words[offb + 2 * i + k // 4], k % 4) for k in range(8)], 0, 7)
+    for i in range(rc if rc > 1 else 0):
+        perm_ok([b(words[offc + i], k) for k in range(4)], 4, 7)
+
+
 def closed_entry_py(n, seed, e):
     """Python restatement of the closed-form schedule for one entry."""
     nq = oracle_lib.n_qubits(n)
