@@ -850,7 +850,11 @@ __device__ __forceinline__ uint32_t qba_add_word(uint32_t base, uint32_t x, int 
 }
 
 __device__ __forceinline__ void qba_lds_add(uint32_t addr, uint32_t v) {
+#ifdef QBA_EXP_NOATOMIC  // experiment builds: the address work without the LDS atomic
+  asm volatile("" ::"v"(addr), "v"(v));
+#else
   atomicAdd((uint32_t *)qba_lds(addr), v);
+#endif
 }
 
 // Count one Q-correlated entry (c0, c1) into the pair bins; hA = LDS byte
@@ -1199,7 +1203,11 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
         }
       }
     }
+#ifdef QBA_EXP_NOSTORE  // experiment builds: the row stores skipped (never true), their transposes kept
+    if (Dp[0][0] == 0x12345678u && Dp[1][1] == 0x9abcdef0u) {
+#else
     if (!TAIL && act) {
+#endif
       uint64_t rbl = 0;  // QBA_SGPR_LEAN: the running row base
       (void)rbl;
 #pragma unroll
