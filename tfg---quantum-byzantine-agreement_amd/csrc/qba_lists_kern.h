@@ -1203,7 +1203,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
         }
       }
     }
-#ifdef QBA_EXP_NOSTORE  // experiment builds: the row stores skipped (never true), their transposes kept
+#ifdef QBA_EXP_NOSTORE  // experiment builds: the row stores and their transposes skipped (never true)
     if (Dp[0][0] == 0x12345678u && Dp[1][1] == 0x9abcdef0u) {
 #else
     if (!TAIL && act) {
