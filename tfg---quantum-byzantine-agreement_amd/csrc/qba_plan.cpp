@@ -191,6 +191,8 @@ static void build_perm_tables(int n, std::vector<uint32_t> &words, uint32_t &ra,
 static bool check_perm_tables(int n, const std::vector<uint32_t> &w, uint32_t ra, uint32_t rb, uint32_t rc,
                               int offB, int offC) {
   const int base = n >= 8 ? 4 : 0;
+  if (w.size() != 4 * (size_t)ra + 2 * (size_t)rb + rc || offB != 4 * (int)ra || offC != offB + 2 * (int)rb)
+    return false;  // A [ra][4], B [rb][2], C [rc]: the layout the kernels index
   auto byte = [&](size_t word, int b) { return (int)((w[word] >> (8 * b)) & 0xffu); };
   for (uint32_t i = 0; i < ra; ++i) {
     uint32_t seen = 0;
