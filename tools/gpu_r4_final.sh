@@ -27,8 +27,10 @@ cp $out/traffic_n11.json $root/profiles/traffic_n11.json  # keyed to this build 
 cd $root
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench_driver.json 2> $out/bench_driver.err
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench_driver2.json 2> $out/bench_driver2.err
+# the count-mode CLI before configs[4]: a process right after that one's 256 GiB
+# teardown waits seconds for device memory (profiles/r4/micro)
+timeout -k 10 300 python -u -m tfg---quantum-byzantine-agreement_amd.tfg 1e9 3 --parties 11 --mode count --seed 11 --timing > $out/cli_count_1e9.txt 2>&1
 for c in 0 1 3 4; do
   timeout -k 10 300 python -u bench.py --config $c > $out/bench_config$c.json 2> $out/bench_config$c.err
 done
-timeout -k 10 300 python -u -m tfg---quantum-byzantine-agreement_amd.tfg 1e9 3 --parties 11 --mode count --seed 11 --timing > $out/cli_count_1e9.txt 2>&1
 timeout -k 10 300 python -u tools/prof_protocol.py 11 1e6 3 5 > $out/protocol_1e6.txt 2>&1
