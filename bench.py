@@ -216,7 +216,7 @@ def issue_roofline(tj, entries, launch_ms):
     top = max(busy, key=busy.get)
     out["binds"] = (f"{top} issue ({busy[top]:.0%} busy; "
                     + ", ".join(f"{k} {v:.0%}" for k, v in busy.items() if k != top)
-                    + ("): neither unit saturated, the rest is LDS / memory latency the 8 waves per SIMD do not hide"
+                    + ("): neither unit saturated, the rest is dependency latency the 8 waves per SIMD do not hide"
                        if busy[top] < 0.8 else "): saturated"))
     return out
 
