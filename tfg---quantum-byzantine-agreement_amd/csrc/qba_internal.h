@@ -26,7 +26,7 @@
     defined(QBA_WIDE_QPT) || defined(QBA_MINW) || defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) ||                \
     defined(QBA_RED_ALL_IN_FLIGHT) || defined(QBA_QUEUE) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) ||      \
     defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) ||               \
-    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N) || defined(QBA_PAIRBINS) || defined(QBA_SAMP_TRIM) || defined(QBA_SPLIT_LAST) || defined(QBA_RANK_MASK) || defined(QBA_PUSH_W2) || defined(QBA_PB_ALIGN) || defined(QBA_DEF_PAIRWISE) || defined(QBA_PB_CHECK_DISTINCT) || defined(QBA_DEF_GTAB) || defined(QBA_DEF_WAVES)
+    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N) || defined(QBA_PAIRBINS) || defined(QBA_SAMP_TRIM) || defined(QBA_SPLIT_LAST) || defined(QBA_RANK_MASK) || defined(QBA_PUSH_W2) || defined(QBA_PB_ALIGN) || defined(QBA_DEF_PAIRWISE) || defined(QBA_PB_CHECK_DISTINCT) || defined(QBA_PB_DRAIN_PRIO) || defined(QBA_DEF_GTAB) || defined(QBA_DEF_WAVES)
 #ifndef QBA_EXPERIMENT_BUILD
 #error "an experiment switch is set without QBA_EXPERIMENT_BUILD (tools/exp/build.sh): not a shippable libqba"
 #endif

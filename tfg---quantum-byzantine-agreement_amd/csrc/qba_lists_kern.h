@@ -48,6 +48,9 @@
 #ifndef QBA_PB_ALIGN  // pair bins: array A 1-KiB aligned, base = one v_and_or
 #define QBA_PB_ALIGN 1
 #endif
+#ifndef QBA_PB_DRAIN_PRIO  // pair-bin drains at raised wave priority
+#define QBA_PB_DRAIN_PRIO 1
+#endif
 #ifndef QBA_PB_CHECK_DISTINCT  // pair bins: per-entry distinctness test + equal-pair slow path (experiment)
 #define QBA_PB_CHECK_DISTINCT 0
 #endif
@@ -929,9 +932,13 @@ __device__ __forceinline__ void qba_q_drain_pb(QbaWaveQ &q, uint32_t nv) {
   typedef uint32_t v2u __attribute__((ext_vector_type(2)));
   const v2u c = *reinterpret_cast<__attribute__((address_space(3))) v2u *>(
       static_cast<uintptr_t>(qba_qpb_addr(q, q.tail + lane)));
+#if QBA_PB_DRAIN_PRIO
   __builtin_amdgcn_s_setprio(2);  // as qba_q_drain
+#endif
   if (nv >= 64 || lane < nv) qba_count_pb<NP>(c.x, c.y, q.hoff);
+#if QBA_PB_DRAIN_PRIO
   __builtin_amdgcn_s_setprio(0);
+#endif
   q.tail += nv;
   q.qn -= nv;
 }
