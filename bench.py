@@ -10,11 +10,13 @@ process per GPU under torch.distributed.run, see launch_ranks) and prints rank
 
 One step (default, --config 2) = one pass of the hot path over this rank's
 shard of sizeL: every entry is Born-sampled from the compiled resource program
-(Philox keyed by the global entry index), its n+1 list bytes are written to
-HBM, and the count-mode checks (isQCorr, P_u, every party's tuple histogram
-and every pairwise collision -- the inputs of consistent()) are accumulated;
-for N > 1 the count histograms are then summed over ranks with one RCCL
-all-reduce.
+(Philox keyed by the global entry index), its n+1 list values are written to
+HBM, and the count-mode checks run on every Q-correlated entry from registers:
+isQCorr (L0 != L1, tfg.py:327), P_u, every party's tuple histogram, and
+Cond3's pairwise test (tfg.py:96-98: the union of the entry's one-hot values
+must have n+1 bits; an entry that fails it counts every equal pair into C) --
+the inputs of consistent(); for N > 1 the count histograms are then summed
+over ranks with one RCCL all-reduce.
 
 Workload (config.workload): BASELINE.json configs[2] -- n = 11 parties,
 3 dishonest, sizeL = 1e9 sharded over 8 GPUs -- i.e. 1.25e8 entries per GPU.
@@ -33,16 +35,19 @@ Other BASELINE.json configs (one JSON line each, one GPU):
               register of the Q circuit, n+1 qubits); GB/s of its fused CX
               pass and the register's preparation time.
 
-roofline.achieved = algorithmic bytes per launch (2(n+1) B per
-entry, lists written once + read once for verification, scored at that even
-though the fused kernel never re-reads them) / the launch's device time,
-measured with HIP events on the stream the kernels run on.  The launch is the
-whole sample_check call: the fused kernel and the slab reduction (qba_k_reduce).
-One event pair brackets the K timed launches (device time / K): an event pair
-around every launch costs ~10 us of GPU time per step (markers between the
-kernels; rocprofv3 trace: 10.4 us gaps before each list kernel, none with
-one pair), which would be charged to the step.  QBA_BENCH_EVENTS=step
-restores the per-launch pairs.
+roofline.achieved = the HBM bytes the fused pass must move per launch -- the
+lists written once ((n+1)/2 B per entry as nibble rows, (n+1) B as byte rows;
+the checks run from registers and never re-read them) -- / the launch's device
+time, measured with HIP events on the stream the kernels run on; frac is that
+over the 8 TB/s peak, a physical fraction (roofline.traffic: the PMC-measured
+bytes of this build, within ~3 % of it).  BASELINE's own scoring convention
+(2(n+1) B per entry: lists written + read back once) is reported beside it as
+roofline.metric_scale.  The launch is the whole sample_check call: the fused
+kernel and the slab reduction (qba_k_reduce).  One event pair brackets the K
+timed launches (device time / K): an event pair around every launch costs
+~10 us of GPU time per step (markers between the kernels; rocprofv3 trace:
+10.4 us gaps before each list kernel, none with one pair), which would be
+charged to the step.  QBA_BENCH_EVENTS=step restores the per-launch pairs.
 """
 from __future__ import annotations
 
@@ -163,6 +168,8 @@ def verify_counts(n, seed, per, world, H, C, P):
     """bench.py's verification block for one set of all-reduced counts."""
     import numpy as np
     offdiag = int(C.sum() - sum(C[:, g, g].sum() for g in range(n + 1)))
+    # offdiag_collisions: equal pairs g != h at Q-correlated entries, found by
+    # the kernel's per-entry Cond3 test (tfg.py:96-98); 0 for honest lists
     out = {"q_entries": int(P.sum()), "offdiag_collisions": offdiag}
     ref = golden_counts(n, seed, per, world)
     if ref is not None:
@@ -352,8 +359,13 @@ def headline(args):
         return
     entries = per * world * args.steps
     value = entries / t_max
-    bytes_per_entry = 2 * (n + 1)
-    achieved = bytes_per_entry * per / (kern_ms * 1e-3) / 1e9
+    bytes_per_entry = 2 * (n + 1)  # BASELINE's scoring convention (metric_scale)
+    row_bytes = (n + 1) / 2 if packed else n + 1  # list bytes per entry as stored
+    # the HBM bytes the pass must move: fused / sample write the lists once,
+    # split writes them and reads them back
+    moved_per_entry = row_bytes * (2 if args.mode == "split" else 1)
+    achieved = moved_per_entry * per / (kern_ms * 1e-3) / 1e9
+    metric_gbs = bytes_per_entry * per / (kern_ms * 1e-3) / 1e9
     traffic, traffic_note, issue = None, "no PMC traffic file for this workload", None
     tp = Path(args.traffic)
     if tp.exists():
@@ -400,17 +412,20 @@ def headline(args):
             "kernel": (f"qba_k_lists_pbdef<{n},*> (list kernel; the previous step's count reduction runs in "
                        "its tail)" if deferred else f"qba_k_lists<{n},1,*> + qba_k_reduce") if args.mode == "fused"
                       else f"qba_k_lists<{n},0,*> + qba_k_lists<{n},2,*> + reduce",
-            "algorithmic_bytes_per_entry": bytes_per_entry, "launch_ms": kern_ms,
-            # the bytes the launch really moves (PMC) over the same time: the fused
-            # kernel never re-reads the lists, so this sits near half of frac
+            "algorithmic_bytes_per_entry": moved_per_entry, "launch_ms": kern_ms,
+            "algorithmic_bytes_note": ("the lists written once as " + ("nibble rows" if packed else "byte rows")
+                                       + (" and read back once (split: sample, then check)" if args.mode == "split"
+                                          else "; the checks run from registers")),
+            # the bytes the launch really moves (PMC) over the same time
             "traffic_gbs": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
             "traffic_frac": traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
             "traffic_source": traffic_note,
+            "metric_scale": {"bytes_per_entry": bytes_per_entry, "achieved_gbs": metric_gbs,
+                             "frac": metric_gbs / HBM_PEAK_GBS,
+                             "note": "BASELINE.md's convention: 2(n+1) B per entry (byte lists written once + "
+                                     "read back once), charged even though the fused pass never re-reads them; "
+                                     "not a physical fraction (can pass 1)"},
             "issue": issue,
-            "note": "achieved/frac count the BASELINE's 24 B/entry (byte lists written + read back once); the "
-                    "fused kernel writes them once and never re-reads"
-                    + (", as nibble rows (6 B/entry at n=11)" if packed else "")
-                    + ", so the bytes HBM really moves are traffic (traffic_gbs / traffic_frac)",
         },
         "verification": verify_counts(n, args.seed, per, world, Hn, Cn, Pn),
         "rank_launch_ms": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
@@ -527,7 +542,7 @@ def config1(args, eng):
     fused(n, args.seed, 0, count, lists, ref)
     torch.cuda.synchronize()
     same = all(torch.equal(x, y) for x, y in zip((counts.H, counts.C, counts.P), (ref.H, ref.C, ref.P)))
-    ach = 24 * count / dev / 1e9
+    ach = (6 if packed else 12) * count / dev / 1e9  # lists written once (the checks run from registers)
     extra = {"ms_per_step": wall * 1e3, "sync_us_per_step": sync_wall * 1e6,
              "reduction": "deferred: step k's counts reduced inside step k+1's list kernel, the last by "
                           "the flush at the end of the graph (qba_sample_check_packed_deferred)",
@@ -539,6 +554,9 @@ def config1(args, eng):
                  f"({args.steps} steps in one hipGraph)",
                  {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                  "algorithmic_bytes_per_entry": 6 if packed else 12,
+                  "metric_scale": {"bytes_per_entry": 24, "achieved_gbs": 24 * count / dev / 1e9,
+                                   "frac": 24 * count / dev / 1e9 / HBM_PEAK_GBS},
                   "note": ("6 MB of nibble-row" if packed else "12 MB of byte-row")
                           + " lists stay in the 256 MB Infinity Cache; launch-bound"}, extra,
                  dtype=_dtype(packed))
@@ -563,18 +581,43 @@ def config3(args, eng, n_inst=4096, count=100_000):
     wall = (time.perf_counter() - t0) / args.steps
     dev = a.elapsed_time(b) * 1e-3 / args.steps
     ent = n_inst * count
-    ach = 16 * ent / dev / 1e9
+    row = (n + 1) / 2 if packed else n + 1  # list bytes per entry, written once
+    ach = row * ent / dev / 1e9
+    # every instance's equal-pair counts (found by the per-entry Cond3 test):
+    # C[u][g][g] = |P_u| on the diagonal, 0 off it for honest lists
     honest = bool((c.C.sum((1, 2, 3)) == c.P.sum(1) * (n + 1)).all().item())
     extra = {"ms_per_step": wall * 1e3, "verification": {"all_instances_collision_free": honest}}
+    if not args.no_cpu_baseline:
+        extra["cpu_baseline"] = cpu_baseline_batched(n, args.seed, count, eng.prepare(n), args.cpu_seconds)
     return _line(args, ent / wall, "entries/s",
                  f"BASELINE configs[3]: {n_inst} independent n=7 instances x sizeL={count} per GPU",
                  {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": ach / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_entry": 16,
-                  "written_gbs": ach / (4 if packed else 2), "written_frac": ach / (4 if packed else 2) / HBM_PEAK_GBS,
-                  "list_layout": "nibble rows (4 B/entry at n=7)" if packed else "byte rows (8 B/entry)",
-                  "note": "BASELINE scores 2(n+1) = 16 B/entry (lists written + read back); the batched "
-                          "kernel writes the lists once and never re-reads them, so frac can pass 1 -- "
-                          "written_gbs is the store stream it actually moves"}, extra, dtype=_dtype(packed))
+                  "frac": ach / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_entry": row,
+                  "metric_scale": {"bytes_per_entry": 16, "achieved_gbs": 16 * ent / dev / 1e9,
+                                   "frac": 16 * ent / dev / 1e9 / HBM_PEAK_GBS,
+                                   "note": "BASELINE's 2(n+1) B per entry (lists written + read back); "
+                                           "the batched kernel writes them once and never re-reads them"},
+                  "list_layout": "nibble rows (4 B/entry at n=7)" if packed else "byte rows (8 B/entry)"},
+                 extra, dtype=_dtype(packed))
+
+
+def cpu_baseline_batched(n, seed, count, info, target_s):
+    """BASELINE.md CPU plan item 3 for configs[3]: the C twin's batched counts
+    (oracle_batched_counts: one instance per OpenMP thread at a time, the same
+    keys and count semantics) over a bounded slice of the 4096 instances."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_lib
+    step = max(oracle_lib.threads(), 1)
+    done, t0 = 0, time.perf_counter()
+    while done < 4096:
+        oracle_lib.batched_counts(n, seed + done, step, count, info["notq"], info["q"], info["closed"])
+        done += step
+        if time.perf_counter() - t0 >= target_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done * count / dt, "unit": "entries/s", "cores": oracle_lib.threads(), "kind": "port",
+            "sample": f"{done} of the 4096 instances (keys seed + [0, {done})) x sizeL={count}, n={n}: C twin "
+                      f"(oracle/sampler_ref.c oracle_batched_counts) sample + count, {dt:.1f} s"}
 
 
 def config4(args, eng):

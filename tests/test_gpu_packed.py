@@ -225,16 +225,94 @@ def test_pairbin_wrap_recount_exact(monkeypatch, packed):
 def test_pairbin_no_recount_at_bench_size(engine):
     """At the headline launch (1.25e8 entries, <= 2^18 per workgroup) no pair
     bin wraps: no workgroup recounts (stats[1] == 0), and the counts of the
-    packed fused pass equal the check-only kernel's (32-bit bins) on its rows."""
+    packed fused pass equal the pair-bin check of its rows and the classic
+    check (32-bit bins) of the same rows unpacked to bytes."""
     n, seed, count = 11, 0x5EED, 125_000_000
     p, c = engine.sample_check_packed(n, seed, 0, count)
     st = engine.last_stats()
     assert st[0] == 0 and st[1] == 0, st
     c2 = engine.check_counts_packed(p, n, count)
-    for a, b in zip(c.numpy(), c2.numpy()):
-        assert np.array_equal(a, b)
+    assert list(engine.last_stats()) == [0, 0]
+    u = engine.unpack(p, n + 1, count)
     del p
+    c3 = engine.check_counts(u, n, count)
+    for a, b, d in zip(c.numpy(), c2.numpy(), c3.numpy()):
+        assert np.array_equal(a, b) and np.array_equal(a, d)
+    del u
     torch.cuda.empty_cache()
+
+
+def _collided(n, count, seed):
+    """Uniform n = 11 lists with equal pairs injected at a third of the
+    Q-correlated entries (random groups g != h >= 2: L_h := L_g)."""
+    rng = np.random.default_rng(seed)
+    L = rng.integers(0, 16, (n + 1, count)).astype(np.uint8)
+    L[1] = np.where(rng.random(count) < 0.5, L[0], L[1])  # ~half not Q-correlated
+    isq = np.nonzero(L[0] != L[1])[0]
+    for k in rng.choice(isq, len(isq) // 3, replace=False):
+        g, h = rng.choice(np.arange(2, n + 1), 2, replace=False)
+        L[h, k] = L[g, k]
+    return L
+
+
+@pytest.mark.parametrize("force,count", [("QBA_PB_MIN_ENTRIES=0", 30_001), ("QBA_PB_MIN_ENTRIES=0", 8),
+                                         ("QBA_PB_MIN_ENTRIES=0", 1_000_003), ("QBA_LIST_GRID=2", 5_000_001)])
+def test_pairbin_check_counts_collisions_exact(monkeypatch, force, count):
+    """Cond3 (tfg.py:96-98) through the pair-bin counter: qba_check_counts_packed
+    at n = 11 counts in pair bins (QbaUsePB), so injected equal pairs drive the
+    counter's distinctness test and its equal-pair slow path (C[u][g][h] in B's
+    upper lanes).  Small and ragged launches (pair bins forced below their
+    threshold) and a wrapping one (two workgroups: recount, stats[1] == 2) are
+    bit-exact against the numpy restatement; uniform lists over [0, 4) make
+    every Q entry collide."""
+    key, val = force.split("=")
+    monkeypatch.setenv(key, val)
+    eng = sub("engine").Engine(0)
+    try:
+        n = 11
+        for L in (_collided(n, count, count), np.random.default_rng(5).integers(0, 4, (n + 1, count)).astype(np.uint8)):
+            d = torch.zeros((n + 1, (count + 4095) // 4096 * 4096), dtype=torch.uint8, device=eng.device)
+            d[:, :count] = torch.from_numpy(L).to(eng.device)
+            c = eng.check_counts_packed(eng.pack(d, n + 1, count), n, count)
+            gH, gC, gP = c.numpy()
+            H, C, P = orc.counts(L, n)
+            assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P)
+            offdiag = int(C.sum() - sum(C[:, g, g].sum() for g in range(n + 1)))
+            assert offdiag > 0 or count < 64
+            st = list(eng.last_stats())
+            assert st == ([0, 2] if key == "QBA_LIST_GRID" else [0, 0]), st
+    finally:
+        eng.close()
+
+
+def test_slab_event_survives_stream_destruction(engine):
+    """A counting call on stream A, A synchronised and destroyed, then counting
+    calls on a new stream B (and deferred ones on C): the slab's ordering event
+    was recorded on A while it existed, so no destroyed stream is touched and
+    every result stays exact (qba_slab_order)."""
+    n, seed, count = 11, 99, 200_003
+    ref = _ref(engine, n, seed, 0, count)
+    a = torch.cuda.Stream()
+    with torch.cuda.stream(a):
+        p, c = engine.sample_check_packed(n, seed, 0, count)
+    a.synchronize()
+    assert _same_counts(c, ref)
+    del a
+    import gc
+    gc.collect()
+    for _ in range(2):
+        b = torch.cuda.Stream()
+        with torch.cuda.stream(b):
+            p2, c2 = engine.sample_check_packed(n, seed, 0, count)
+            p3, c3 = engine.sample_check_packed(n, seed, 0, count, deferred=True)
+            engine.flush_deferred()
+        b.synchronize()
+        assert _same_counts(c2, ref) and _same_counts(c3, ref)
+        assert np.array_equal(_unpack(p3, count), ref)
+        del b
+        gc.collect()
+    p4, c4 = engine.sample_check_packed(n, seed, 0, count)
+    assert _same_counts(c4, ref)
 
 
 @pytest.mark.parametrize("packed", [True, False])

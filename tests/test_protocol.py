@@ -208,3 +208,26 @@ def test_local_world_device_row_messages():
 
     with pytest.raises(Exception):
         w2.run(bad)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["n"] == 3][:3], ids=lambda c: c["name"])
+def test_protocol_out_of_range_injection_rows_equal_wire(case):
+    """Injected values >= w: the wire carries nq bits per value (tfg.py:84,
+    128-129), so the in-process device-row run must see the values the wire
+    run decodes -- both runs agree on every outcome."""
+    L = LISTS[case["name"]].astype(np.int64).copy()
+    rng = np.random.default_rng(7)
+    w = 1 << sub("resource").n_qubits(case["n"])
+    pick = rng.choice(L.size, 40, replace=False)
+    L.flat[pick] += w * rng.integers(1, 4, 40)  # same low nq bits, out of range
+    protocol = sub("protocol")
+
+    def run(engine, **kw):
+        return protocol.run_local(case["n"], case["sizeL"], case["nDishonest"], engine, seed=case["seed"],
+                                  lists=L, timeout=60, party_kwargs=kw or None)
+
+    rows, wire = run(_RowEngine()), run(OracleEngine(), wire=True)
+    assert (rows.error, rows.result, rows.V, rows.accept, rows.reject) == \
+        (wire.error, wire.result, wire.V, wire.accept, wire.reject)
+    # and both equal the in-range lists' run (the low nq bits are unchanged)
+    _compare(rows, case["exact"])

@@ -26,7 +26,7 @@
     defined(QBA_WIDE_QPT) || defined(QBA_MINW) || defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) ||                \
     defined(QBA_RED_ALL_IN_FLIGHT) || defined(QBA_QUEUE) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) ||      \
     defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) ||               \
-    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N) || defined(QBA_PAIRBINS) || defined(QBA_SAMP_TRIM) || defined(QBA_SPLIT_LAST) || defined(QBA_RANK_MASK) || defined(QBA_PUSH_W2) || defined(QBA_PB_ALIGN) || defined(QBA_DEF_PAIRWISE) || defined(QBA_PB_CHECK_DISTINCT) || defined(QBA_PB_DRAIN_PRIO) || defined(QBA_DEF_GTAB) || defined(QBA_DEF_WAVES)
+    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N) || defined(QBA_PAIRBINS) || defined(QBA_SAMP_TRIM) || defined(QBA_SPLIT_LAST) || defined(QBA_RANK_MASK) || defined(QBA_PUSH_W2) || defined(QBA_PB_ALIGN) || defined(QBA_DEF_PAIRWISE) || defined(QBA_PB_DRAIN_PRIO) || defined(QBA_DEF_GTAB) || defined(QBA_DEF_WAVES)
 #ifndef QBA_EXPERIMENT_BUILD
 #error "an experiment switch is set without QBA_EXPERIMENT_BUILD (tools/exp/build.sh): not a shippable libqba"
 #endif
@@ -224,16 +224,21 @@ struct qba_ctx {
   // recorded inside a capture, with that capture's id
   int pend_captured = 0;
   unsigned long long pend_capture_id = 0;
-  // the stream of the slab's last user (qba_slab_order): a counting launch on
-  // another stream is ordered after it
-  hipStream_t slab_stream = nullptr;
-  bool slab_used = false;
+  // the slab's last user (qba_slab_order / qba_slab_done): an event recorded
+  // on its stream after its launches, and that stream's handle as a VALUE only
+  // (compared, never passed to HIP: the stream may be destroyed since); a
+  // counting launch on another stream waits for the event
+  hipEvent_t slab_ev = nullptr;
+  uintptr_t slab_last = 0;
+  bool slab_ev_set = false;
 };
 // Capture state of a stream: 1 capturing (its capture id in *id), 0 not.
 int qba_capture_of(hipStream_t s, unsigned long long *id);
 // Order a counting launch on `stream` after the slab's previous user on
-// another stream (an event, or nothing when that stream is idle).
+// another stream (waits for the event qba_slab_done recorded), and record
+// the event after the launches of a call that used the slab.
 int qba_slab_order(qba_ctx *ctx, hipStream_t stream);
+int qba_slab_done(qba_ctx *ctx, hipStream_t stream);
 void qba_rccl_release(qba_ctx *ctx);
 
 int qba_ensure_slab(qba_ctx *ctx, size_t bytes);

@@ -172,18 +172,24 @@ static int pend_capture_ok(qba_ctx *ctx, hipStream_t s) {
 // Only eager streams are ordered here: inside a capture the graph's own
 // dependencies order its nodes, and across a capture boundary the caller
 // synchronises (include/qba.h) -- an eager event cannot be waited on by a
-// capturing stream.  The capturing stream is tested first, so no other
-// stream is touched while one captures.
+// capturing stream, and a captured launch records no event.  The previous
+// user's stream is never touched: the event was recorded on it while it was
+// known to exist (qba_slab_done), so destroying that stream since is safe.
 int qba_slab_order(qba_ctx *ctx, hipStream_t stream) {
   unsigned long long id = 0;
-  if (ctx->slab_used && ctx->slab_stream != stream && !qba_capture_of(stream, &id) &&
-      !qba_capture_of(ctx->slab_stream, &id)) {
-    if (!ctx->def_ev) QBA_HIP(hipEventCreateWithFlags(&ctx->def_ev, hipEventDisableTiming));
-    QBA_HIP(hipEventRecord(ctx->def_ev, ctx->slab_stream));
-    QBA_HIP(hipStreamWaitEvent(stream, ctx->def_ev, 0));
-  }
-  ctx->slab_stream = stream;
-  ctx->slab_used = true;
+  if (ctx->slab_ev_set && ctx->slab_last != reinterpret_cast<uintptr_t>(stream) && !qba_capture_of(stream, &id))
+    QBA_HIP(hipStreamWaitEvent(stream, ctx->slab_ev, 0));
+  return QBA_OK;
+}
+
+int qba_slab_done(qba_ctx *ctx, hipStream_t stream) {
+  unsigned long long id = 0;
+  ctx->slab_ev_set = false;
+  if (qba_capture_of(stream, &id)) return QBA_OK;
+  if (!ctx->slab_ev) QBA_HIP(hipEventCreateWithFlags(&ctx->slab_ev, hipEventDisableTiming));
+  QBA_HIP(hipEventRecord(ctx->slab_ev, stream));
+  ctx->slab_last = reinterpret_cast<uintptr_t>(stream);
+  ctx->slab_ev_set = true;
   return QBA_OK;
 }
 
@@ -196,7 +202,7 @@ int qba_flush_pending(qba_ctx *ctx, hipStream_t next) {
   int (*f)(qba_ctx *) = pd.flush;
   int rc = f(ctx);
   pd.flush = nullptr;
-  if (rc) return rc;
+  if (rc || (rc = qba_slab_done(ctx, pd.stream))) return rc;  // the reduction read the slab
   if (next != pd.stream) {  // the slab may be rewritten on `next`: after this reduction
     if (!ctx->def_ev) QBA_HIP(hipEventCreateWithFlags(&ctx->def_ev, hipEventDisableTiming));
     QBA_HIP(hipEventRecord(ctx->def_ev, pd.stream));

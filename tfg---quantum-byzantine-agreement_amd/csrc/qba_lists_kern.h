@@ -51,9 +51,6 @@
 #ifndef QBA_PB_DRAIN_PRIO  // pair-bin drains at raised wave priority
 #define QBA_PB_DRAIN_PRIO 1
 #endif
-#ifndef QBA_PB_CHECK_DISTINCT  // pair bins: per-entry distinctness test + equal-pair slow path (experiment)
-#define QBA_PB_CHECK_DISTINCT 0
-#endif
 #ifndef QBA_RANK_MASK  // not-Q entries read table entry 0 (LDS broadcast) instead of a random one
 #define QBA_RANK_MASK 1
 #endif
@@ -468,6 +465,15 @@ __device__ __forceinline__ uint32_t qba_pk_onehot(uint32_t amt, uint32_t one) {
   return r;
 }
 
+// lo | hi of a word's two 16-bit halves in ONE op (an SDWA v_or with the
+// upper half zeroed): the union of two 16-bit one-hot sets
+__device__ __forceinline__ uint32_t qba_fold16(uint32_t u) {
+  uint32_t r;
+  asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
+      : "=v"(r) : "v"(u));
+  return r;
+}
+
 typedef __attribute__((address_space(3))) uint32_t qba_lds_u32;  // LDS word (32-bit address)
 
 // base + byte b of x in one VALU op (v_add_u32 with an SDWA byte select)
@@ -493,13 +499,10 @@ __device__ __forceinline__ uint32_t qba_byte_of(int g, uint32_t w0, uint32_t w1,
 // count one entry (group g = byte g % 4 of D[g / 4])
 //   Q-correlated iff L0 != L1 (tfg.py:327); u = L1 (tfg.py:182);
 //   H[u][g][L_g] += 1 for every g; C[u][g][h] += 1 for every equal pair --
-//   the pair loop runs only when the entry's distinct-value count (union of
-//   16-bit one-hots) is below n+1.  DIST: the entry comes from the closed-form
-//   sampler, whose Q entries hold n+1 distinct values by construction (the
-//   stage tables are permutations, checked by qba_plan): no C bin can count,
-//   so the test is skipped (see qba_count_pb).
+//   every counted entry is tested (its distinct-value count: the union of
+//   16-bit one-hots), the pair loop runs only when that count is below n+1.
 // ---------------------------------------------------------------------------
-template <int NP, bool DIST = false>
+template <int NP>
 __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uint32_t one,
                                             uint32_t *hist, bool in_range, bool known_q = false,
                                             uint32_t hoff = 0xffffffffu) {
@@ -550,10 +553,8 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
       }
     }
   }
-#ifdef QBA_EXP_NOSEEN
-  return;
-#endif
-  if constexpr (DIST && !QBA_PB_CHECK_DISTINCT) return;
+  // Cond3 (tfg.py:96-98): distinct iff the union of the values' 16-bit
+  // one-hots (two per v_pk_lshlrev_b16) has n+1 bits
   uint32_t U = 0;
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) {
@@ -564,13 +565,7 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
     if (4 * i + 3 < C::G) mq |= 0xffff0000u;
     U |= (qba_pk_onehot(D[i], one) & mp) | (qba_pk_onehot(D[i] >> 8, one) & mq);
   }
-  {  // lo | hi in ONE op: an SDWA or with the upper half zeroed (was lshr + and_or)
-    uint32_t r;
-    asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
-        : "=v"(r) : "v"(U));
-    U = r;
-  }
-  if (__popc(U) != C::G) {  // some pair collides: exact slow path
+  if (__popc(qba_fold16(U)) != C::G) {  // some pair collides: exact slow path
     // a compact loop (values picked by selects, no private array): this
     // path is rare and unrolling it would multiply the kernel's code size
     uint32_t *c = hist + C::HBL + l1r * C::CP;
@@ -754,7 +749,7 @@ __device__ __forceinline__ uint32_t qba_queue_base(uint32_t *hist) {
 // Count the nv (<= 64) oldest queued entries, one per lane.  TRUSTED: the
 // values were produced by this kernel's sampler, masked to nq bits, so
 // Cond2's range test cannot fail and is skipped (check-only launches keep it).
-template <int NP, bool TRUSTED, bool DIST = false>
+template <int NP, bool TRUSTED>
 __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_t nv) {
   constexpr int ND = CF<NP>::ND;
   const uint32_t lane = __lane_id();
@@ -767,7 +762,7 @@ __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_
   __builtin_amdgcn_s_setprio(2);
 #pragma unroll
   for (int i = 0; i < ND; ++i) D[i] = *qba_lds(a + i * QBA_QCAP * 4);
-  if (nv >= 64 || lane < nv) qba_count_d<NP, DIST>(D, 0x00010001u, hist, TRUSTED, true, q.hoff);
+  if (nv >= 64 || lane < nv) qba_count_d<NP>(D, 0x00010001u, hist, TRUSTED, true, q.hoff);
   __builtin_amdgcn_s_setprio(0);
   q.tail += nv;
   q.qn -= nv;
@@ -776,7 +771,7 @@ __device__ __forceinline__ void qba_q_drain(QbaWaveQ &q, uint32_t *hist, uint32_
 // Append the lanes' entries with isq set (in lane order) and count a full
 // batch of 64 as soon as one is queued.  Slot = tail + qn + the number of
 // queued lanes below this one (mbcnt adds the base for free).
-template <int NP, bool TRUSTED, bool DIST = false>
+template <int NP, bool TRUSTED>
 __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], bool isq,
                                            uint32_t *hist) {
   constexpr int ND = CF<NP>::ND;
@@ -790,7 +785,7 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
     for (int i = 0; i < ND; ++i) *qba_lds(a + i * QBA_QCAP * 4) = D[i];
   }
   q.qn += (uint32_t)__popcll(m);
-  if (q.qn >= 64) qba_q_drain<NP, TRUSTED, DIST>(q, hist, 64u);
+  if (q.qn >= 64) qba_q_drain<NP, TRUSTED>(q, hist, 64u);
 }
 
 // ---------------------------------------------------------------------------
@@ -837,9 +832,12 @@ struct QbaPB {
   static constexpr int AREA = WORDS + MISC;
   static constexpr int QSLOT = 8;          // queue bytes per entry
 };
-template <int NP, int MODE, int SAMP>
-struct QbaUsePB {  // the fused closed-form n = 11 kernel counts with pair bins
-  static constexpr bool value = QBA_PAIRBINS && NP == 11 && MODE == 1 && SAMP == QBA_S_CLOSED;
+// the kernels that count with pair bins: the fused closed-form n = 11 kernel
+// and the n = 11 check of nibble rows (every value < 16 = w, so no range test)
+template <int NP, int MODE, int SAMP, int PK>
+struct QbaUsePB {
+  static constexpr bool value =
+      QBA_PAIRBINS && NP == 11 && ((MODE == 1 && SAMP == QBA_S_CLOSED) || (MODE == 2 && PK == 1));
 };
 
 // base + 16-bit half h of x in one VALU op (v_add_u32 with an SDWA word select)
@@ -883,24 +881,23 @@ __device__ __forceinline__ void qba_count_pb(uint32_t c0, uint32_t c1, uint32_t 
   qba_lds_add(qba_add_word(hb, E1, 1), 0x10000u);        // (6,7)   A lane 2
   qba_lds_add(qba_add_word(hb, E2, 0), 0x1000000u);      // (8,9)   A lane 3
   qba_lds_add(qba_add_word(hb, E2, 1) + B, 0x1u);        // (10,11) B lane 0
-#if QBA_PB_CHECK_DISTINCT
-  // distinctness (Cond 3 fast path): union of the 12 one-hots, 2 per op.
-  // Not needed in the shipped build: pair bins count only the closed-form
-  // sampler's own entries (QbaUsePB), whose 12 values r ^ pi(g) are distinct
-  // for every Q entry because the stage tables are permutations -- which
-  // qba_plan checks when it builds them (check_perm_tables) -- so every C bin
-  // stays 0 without this test (-12 VALU per Q entry).
+#ifdef QBA_EXP_NOCOND3  // experiment builds: the test below skipped (A/B of its cost; results wrong on collisions)
+  return;
+#endif
+  // Cond3 (tfg.py:96-98) on every counted entry: its 12 values are pairwise
+  // distinct iff the union of their 16-bit one-hots has 12 bits.  Each
+  // v_pk_lshlrev_b16 makes two one-hots from the low nibbles of the two
+  // halves of its amount: c0 -> groups 0, 2; c0 >> 4 -> 4, 6; c0 >> 8 -> 1,
+  // 3; c0 >> 12 -> 5, 7; c1 -> 8, 10; c1 >> 8 -> 9, 11.
   const uint32_t one = 0x00010001u;
-  uint32_t U = qba_pk_onehot(c0, one) | qba_pk_onehot(c0 >> 4, one) | qba_pk_onehot(c0 >> 8, one);
-  U |= qba_pk_onehot(c0 >> 12, one) | qba_pk_onehot(c1, one) | qba_pk_onehot(c1 >> 8, one);
-  {
-    uint32_t r;
-    asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
-        : "=v"(r) : "v"(U));
-    U = r;
-  }
-  if (__popc(U) != QCfg<NP>::G) {  // some pair collides: exact slow path (never for sampled lists)
-    const uint32_t w0 = c0 & 0x0f0f0f0fu, w1 = (c0 >> 4) & 0x0f0f0f0fu, w2 = c1;
+  const uint32_t s4 = c0 >> 4;
+  uint32_t U = qba_pk_onehot(c0, one) | qba_pk_onehot(s4, one) | qba_pk_onehot(c0 >> 8, one);
+  U |= qba_pk_onehot(s4 >> 8, one) | qba_pk_onehot(c1, one) | qba_pk_onehot(c1 >> 8, one);
+  if (__popc(qba_fold16(U)) != QCfg<NP>::G) {  // some pair collides: exact slow path
+    // C[u][k] for every equal pair k = pidx(g, h): B lanes 1-3 of the word
+    // (x_g = k & 15, u, x_h = u ^ (1 + k / 16)), a word no Q entry's group 0
+    // uses (x_h != u; qba_pb_flush reads them back)
+    const uint32_t w0 = c0 & 0x0f0f0f0fu, w1 = s4 & 0x0f0f0f0fu, w2 = c1;
     const uint32_t u = __builtin_amdgcn_ubfe(c0, 8, 4);
     int k = 0;
 #pragma nounroll
@@ -912,7 +909,6 @@ __device__ __forceinline__ void qba_count_pb(uint32_t c0, uint32_t c1, uint32_t 
           qba_lds_add(hA + B + 4 * (uint32_t)((k & 15) + 16 * u + 256 * (u ^ (1 + (k >> 4)))), 0x100u);
     }
   }
-#endif
 }
 
 // the queue's 8-B form of an entry in the byte layout (values < 16)
@@ -962,21 +958,21 @@ __device__ __forceinline__ void qba_q_push_pb(QbaWaveQ &q, const uint32_t (&D)[C
 
 // Push (the wave queue) / count one entry directly (tails) with the counting
 // scheme CNT (0: classic 32-bit bins in `hist`, 1: pair bins, hist = array A).
-template <int NP, bool TRUSTED, int CNT, bool DIST = false>
+template <int NP, bool TRUSTED, int CNT>
 __device__ __forceinline__ void qba_push(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], bool isq, uint32_t *hist) {
   if constexpr (CNT == 1)
     qba_q_push_pb<NP>(q, D, isq);
   else
-    qba_q_push<NP, TRUSTED, DIST>(q, D, isq, hist);
+    qba_q_push<NP, TRUSTED>(q, D, isq, hist);
 }
-template <int NP, int CNT, bool DIST = false>
+template <int NP, int CNT>
 __device__ __forceinline__ void qba_count_one(const uint32_t (&D)[CF<NP>::ND], uint32_t *hist) {
   if constexpr (CNT == 1) {
     if ((D[0] & 0xffu) == ((D[0] >> 8) & 0xffu)) return;  // not Q-correlated (tfg.py:327)
     const uint2 c = qba_pb_pack<NP>(D);
     qba_count_pb<NP>(c.x, c.y, (uint32_t)(uintptr_t)(qba_lds_u32 *)hist);
   } else {
-    qba_count_d<NP, DIST>(D, 0x00010001u, hist, true);
+    qba_count_d<NP>(D, 0x00010001u, hist, true);
   }
 }
 
@@ -1049,7 +1045,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
           const uint32_t xq = (row[k][0] ^ row[k][1]) & (act ? 0xffffffffu : 0u);
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            qba_push<NP, MODE == 1, CNT, SAMP == QBA_S_CLOSED>(*wq, D[j], (xq & (0xffu << (8 * j))) != 0u, hist);
+            qba_push<NP, MODE == 1, CNT>(*wq, D[j], (xq & (0xffu << (8 * j))) != 0u, hist);
         } else if constexpr (CNT == 1) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -1135,7 +1131,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
   constexpr int ND = CF<NP>::ND;
   static_assert(QPT == 1 || QPT == 2, "packed rows: QPT 1 or 2");
   static_assert(!TAIL || QPT == 1, "tail quads are single");
-  static_assert(CNT == 0 || MODE == 1, "pair bins count the fused kernel's own lists only");
+  static_assert(CNT == 0 || MODE != 0, "pair bins count");
   static_assert(C::W <= 16, "a value must fit a nibble");
   typedef __attribute__((address_space(1))) uint32_t GU;
   const int valid = !TAIL ? 4 : ((count - c0) >= 4 ? 4 : (int)(count - c0));
@@ -1176,7 +1172,11 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
                D[1][i], D[2][i], D[3][i]);
       if constexpr (WQ) {  // the caller's queue (never null)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) qba_q_push<NP, false>(*wq, D[j], qba_isq_d<NP>(D[j], am), hist);
+        for (int j = 0; j < 4; ++j) qba_push<NP, false, CNT>(*wq, D[j], qba_isq_d<NP>(D[j], am), hist);
+      } else if constexpr (CNT == 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < (TAIL ? valid : 4)) qba_count_one<NP, 1>(D[j], hist);
       } else {
         qba_count_quad<NP>(D, TAIL ? valid : 4, hist, row[k]);
       }
@@ -1200,13 +1200,13 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
           for (int p = 0; p < 2; ++p) {
             const uint32_t w0 = Dp[2 * k + p][0];
             const uint32_t x = (w0 ^ (w0 >> 8)) & am;
-            qba_push<NP, true, CNT, SAMP == QBA_S_CLOSED>(*wq, D[2 * p], (x & 0x0fu) != 0u, hist);
-            qba_push<NP, true, CNT, SAMP == QBA_S_CLOSED>(*wq, D[2 * p + 1], x > 0x0fu, hist);
+            qba_push<NP, true, CNT>(*wq, D[2 * p], (x & 0x0fu) != 0u, hist);
+            qba_push<NP, true, CNT>(*wq, D[2 * p + 1], x > 0x0fu, hist);
           }
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (j < valid) qba_count_one<NP, CNT, SAMP == QBA_S_CLOSED>(D[j], hist);
+            if (j < valid) qba_count_one<NP, CNT>(D[j], hist);
         }
       }
     }
@@ -1506,7 +1506,7 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
       if constexpr (CNT)
         qba_q_drain_pb<NP>(wq, wq.qn < 64 ? wq.qn : 64u);
       else
-        qba_q_drain<NP, MODE == 1, MODE == 1 && SAMP == QBA_S_CLOSED>(wq, hist, wq.qn < 64 ? wq.qn : 64u);
+        qba_q_drain<NP, MODE == 1>(wq, hist, wq.qn < 64 ? wq.qn : 64u);
     }
   } else {
     for (uint32_t u = u0; u < nunits; u += ustride)
@@ -1586,7 +1586,7 @@ __global__ void QBA_LISTS_BOUNDS
     qba_k_lists(const QbaProgramSet *__restrict__ ps, uint32_t k0, uint32_t k1, uint64_t first,
                 uint32_t count, uint8_t *__restrict__ lists, uint64_t ld,
                 uint32_t *__restrict__ slab, QbaZero zero) {
-  static_assert(!CNT || QbaUsePB<NP, MODE, SAMP>::value, "pair bins: the fused closed-form n = 11 kernel only");
+  static_assert(!CNT || QbaUsePB<NP, MODE, SAMP, PK>::value, "pair bins: the n = 11 kernels of QbaUsePB only");
   qba_lists_body<NP, MODE, SAMP, QPT, PK, QBA_LBLOCK, CNT>(ps, k0, k1, first, count, lists, ld, slab, zero, 0u);
 }
 
@@ -1793,7 +1793,7 @@ __global__ void __launch_bounds__(QBA_BLOCK)
       qba_step_l<NP, 1, SAMP, QPT, false, PK, true>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl,
                                               L, ld, hist, &wq, act);
     }
-    while (wq.qn) qba_q_drain<NP, true, SAMP == QBA_S_CLOSED>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
+    while (wq.qn) qba_q_drain<NP, true>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
 #else
     for (uint32_t u = threadIdx.x; u < nunits; u += QBA_BLOCK)
       qba_step_l<NP, 1, SAMP, QPT, false, PK>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,
@@ -1997,11 +1997,13 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     if (int rc = check_closed<NP>(hs)) return rc;
     lds += table_lds<NP>(hs, samp);
   }
-  // the fused closed-form kernel counts with pair bins (QbaPB) when the
-  // launch is large enough to repay their flush (a fixed ~2 us per launch:
-  // 1e6 entries 17.7 vs 15.0 us, 1.25e8 entries 298 vs 313 us,
-  // profiles/r4/small_launch); QBA_LIST_GRID (tests) forces them
-  const bool pb = QbaUsePB<NP, 1, QBA_S_CLOSED>::value && L.mode == 1 && samp == QBA_S_CLOSED &&
+  // the fused closed-form kernel and the check of nibble rows count with
+  // pair bins (QbaPB, n = 11) when the launch is large enough to repay their
+  // flush (a fixed ~2 us per launch: 1e6 entries 17.7 vs 15.0 us, 1.25e8
+  // entries 298 vs 313 us, profiles/r4/small_launch); QBA_LIST_GRID (tests)
+  // forces them
+  const bool pb = ((L.mode == 1 && QbaUsePB<NP, 1, QBA_S_CLOSED, 0>::value && samp == QBA_S_CLOSED) ||
+                   (L.mode == 2 && QbaUsePB<NP, 2, QBA_S_GENERAL, 1>::value && L.packed)) &&
                   (L.count >= ctx->pb_min || ctx->list_grid > 0);
   if (pb) {
     lds += 1024 + (size_t)QbaPB::AREA * sizeof(uint32_t) + (size_t)(QBA_LBLOCK / 64 + 1) * QBA_QCAP * QbaPB::QSLOT;
@@ -2029,10 +2031,14 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   const void *kern = nullptr;
   if (L.mode == 2) {
     kern = QBA_K(2, QBA_S_GENERAL);
+    if constexpr (QbaUsePB<NP, 2, QBA_S_GENERAL, 1>::value)
+      if (pb)
+        kern = wide ? (const void *)qba_k_lists<NP, 2, QBA_S_GENERAL, 2, 1, 1>
+                    : (const void *)qba_k_lists<NP, 2, QBA_S_GENERAL, 1, 1, 1>;
   } else if (samp == QBA_S_CLOSED) {
     if constexpr (NP <= QBA_CLOSED_MAX_N) {
       kern = L.mode == 0 ? QBA_K(0, QBA_S_CLOSED) : QBA_K(1, QBA_S_CLOSED);
-      if constexpr (QbaUsePB<NP, 1, QBA_S_CLOSED>::value)
+      if constexpr (QbaUsePB<NP, 1, QBA_S_CLOSED, 0>::value)
         if (pb)
           kern = L.packed ? (wide ? (const void *)qba_k_lists<NP, 1, QBA_S_CLOSED, 2, 1, 1>
                                   : (const void *)qba_k_lists<NP, 1, QBA_S_CLOSED, 1, 1, 1>)
@@ -2050,16 +2056,20 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   int cap = 0;
   int grid = grid_for(ctx, kern, lds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1, &cap);
   if (ctx->list_grid > 0 && grid > ctx->list_grid) grid = ctx->list_grid;  // tests (QBA_LIST_GRID)
-  if (pb && !ctx->list_grid && L.count > (uint64_t)cap * QBA_PB_BUDGET) {
-    // at most QBA_PB_BUDGET entries per workgroup and launch (QbaPB): later
-    // parts accumulate; part boundaries are multiples of 2^18 entries, so the
-    // row alignment and the pair parity of `first` are those of the call
-    const uint64_t part = (uint64_t)cap * QBA_PB_BUDGET;
+  // pair bins: at most QBA_PB_BUDGET entries per workgroup and launch (QbaPB;
+  // a grid capped by QBA_LIST_GRID -- tests that force wraps -- at most 2^23,
+  // so group 0's 24-bit total stays exact)
+  const uint64_t pb_part = ctx->list_grid ? (uint64_t)grid << 23 : (uint64_t)cap * QBA_PB_BUDGET;
+  if (pb && L.count > pb_part) {
+    // later parts accumulate; part boundaries are multiples of 2^18 entries,
+    // so the row alignment and the pair parity of `first` are those of the
+    // call; only the last part of a deferred call defers its reduction
+    const uint64_t part = pb_part;
     QbaLaunch S = L;
-    S.defer = 0;
     int rc = QBA_OK;
     for (uint64_t done = 0; !rc && done < L.count; done += S.count) {
       S.count = L.count - done < part ? L.count - done : part;
+      S.defer = done + S.count >= L.count ? L.defer : 0;
       S.first = L.first + done;
       S.lists = L.lists + (L.packed ? done >> 1 : done);
       S.accumulate = done ? 1 : L.accumulate;
@@ -2081,7 +2091,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   const void *kd = nullptr;
   // a large pair-bin launch defers into its own tail (qba_k_lists_pbdef)
   const bool pbd = pb && L.defer && L.mode == 1;
-  if constexpr (QbaUsePB<NP, 1, QBA_S_CLOSED>::value)
+  if constexpr (QbaUsePB<NP, 1, QBA_S_CLOSED, 0>::value)
     if (pbd)
       kd = L.packed ? (wide ? (const void *)qba_k_lists_pbdef<NP, 2, 1> : (const void *)qba_k_lists_pbdef<NP, 1, 1>)
                     : (wide ? (const void *)qba_k_lists_pbdef<NP, QBA_WIDE_QPT, 0>
@@ -2158,9 +2168,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     pd.stream = L.stream;
     ctx->pend_captured = cap;
     ctx->pend_capture_id = cid;
-    ctx->slab_stream = L.stream;
-    ctx->slab_used = true;
-    return QBA_OK;
+    return qba_slab_done(ctx, L.stream);
   }
   if (L.mode != 0) {
     if (int rc = qba_flush_pending(ctx, L.stream)) return rc;
@@ -2183,7 +2191,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   const dim3 rgrid((C::NBP / 4 + 255) / 256, (grid + QBA_RED_ROWS - 1) / QBA_RED_ROWS);
   hipLaunchKernelGGL(qba_k_reduce<NP>, rgrid, dim3(256), 0, L.stream, slab, grid, L.H, L.C, L.P, L.stats);
   QBA_HIP(hipGetLastError());
-  return QBA_OK;
+  return qba_slab_done(ctx, L.stream);
 }
 
 template <int NP>

@@ -405,9 +405,12 @@ class Party:
         n, sl = self.n, self.sizeL
         if self.inject is None:
             return self.engine.sample(n, self.seed, 0, sl)
-        arr = np.ascontiguousarray(self.inject, dtype=np.uint8)
+        arr = np.asarray(self.inject)
         if arr.shape != (n + 1, sl):
             raise ValueError(f"injected lists must have shape {(n + 1, sl)}")
+        # the wire carries nq bits per value (rawS, tfg.py:84; measure_to_ints,
+        # tfg.py:128-129): the device rows hold what the wire run decodes
+        arr = np.ascontiguousarray(arr.astype(np.int64) & ((1 << self.nq) - 1), dtype=np.uint8)
         return self.engine.to_device(arr)
 
     def _decode(self, raw):

@@ -41,7 +41,8 @@ known = (n + 1) * per // (2 if layout == "packed" else 1)
 out = {"n": n, "per_launch_entries": per, "mode": mode, "layout": layout,
        "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
        "write_calibration": {"known_list_bytes": known, "write_over_known": write / known},
-       "algorithmic_bytes_per_launch": 2 * (n + 1) * per,
+       "algorithmic_bytes_per_launch": known,  # the lists written once (bench.py roofline.achieved)
+       "metric_scale_bytes_per_launch": 2 * (n + 1) * per,  # BASELINE's 2(n+1) B per entry convention
        "source": str(root), "kernel": f"qba_k_lists<{n},1,*>",
        "issue_counters_per_launch": issue,
        # the library the counters were read from: bench.py drops the figure for any other build
