@@ -28,11 +28,55 @@ from oracle_engine import OracleEngine  # noqa: E402
 STATS_TAG = 30_000  # above every protocol tag (EpochComm: 256 * epochs + 6 + 2|L|)
 
 
+class MpiLink:
+    """tfg.count_owners' group seam for the CPU test: the id is 128 random
+    bytes; the all-reduce sums the owners' buffers over MPI point-to-point
+    (owner 0 gathers, adds, sends the sum back) and checks that every owner
+    joined with the id owner 0 made."""
+
+    TAG = 30_100
+
+    def __init__(self, world, mpi, owners):
+        self.world, self.mpi, self.owners = world, mpi, owners
+
+    def unique_id(self) -> bytes:
+        import os
+        return os.urandom(128)
+
+    def allreduce(self, eng, uid, owners, rank):
+        assert owners == self.owners
+        world, mpi, ids = self.world, self.mpi, np.frombuffer(uid, np.uint8).copy()
+
+        def run(flat):
+            flat = np.ascontiguousarray(np.asarray(flat, dtype=np.int64))
+            if rank != 0:
+                world.Send([ids, mpi.INT], dest=0, tag=self.TAG)
+                world.Send([flat, mpi.INT], dest=0, tag=self.TAG + 1)
+                out = np.empty_like(flat)
+                world.Recv([out, mpi.INT], source=0, tag=self.TAG + 2)
+                return out
+            total = flat.copy()
+            for r in range(1, owners):
+                other = np.empty_like(ids)
+                world.Recv([other, mpi.INT], source=r, tag=self.TAG)
+                assert np.array_equal(other, ids), f"owner {r} joined with another id"
+                part = np.empty_like(flat)
+                world.Recv([part, mpi.INT], source=r, tag=self.TAG + 1)
+                total += part
+            for r in range(1, owners):
+                world.Send([total, mpi.INT], dest=r, tag=self.TAG + 2)
+            return total
+        return run
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("case")
     ap.add_argument("--rounds", choices=["epoch", "reference"], default="epoch")
     ap.add_argument("--mode", choices=["exact", "count"], default="exact")
+    ap.add_argument("--owners", type=int, default=0,
+                    help="count mode: G shard owners set up by tfg.count_owners (the mpiexec GPU-owner "
+                         "path) with the numpy engine and an all-reduce over MPI in place of RCCL")
     a = ap.parse_args()
     comm_mod = importlib.import_module(f"{PKG}.comm")
     protocol = importlib.import_module(f"{PKG}.protocol")
@@ -49,8 +93,13 @@ def main():
     comm = comm_mod.EpochComm(world) if a.rounds == "epoch" else world
     rank = world.Get_rank()
     cls = countmode.CountParty if a.mode == "count" else protocol.Party
-    p = cls(comm, case["sizeL"], case["nDishonest"], OracleEngine(), np.random.RandomState(case["seed"] * 1000 + rank),
-            None, lists, case["seed"])
+    eng, kw = OracleEngine(), {}
+    if a.owners:
+        tfg = importlib.import_module(f"{PKG}.tfg")
+        eng, kw = tfg.count_owners(world, MPI, a.owners, lambda dev: OracleEngine(), MpiLink(world, MPI, a.owners))
+        assert (eng is None) == (rank >= a.owners) and ("counter" in kw) == (a.owners > 1 and rank < a.owners)
+    p = cls(comm, case["sizeL"], case["nDishonest"], eng, np.random.RandomState(case["seed"] * 1000 + rank),
+            None, lists, case["seed"], **kw)
     p.tolerate_empty_vi = True
     res = p.run()
     vi = sorted(int(x) for x in p.Vi) if rank > 1 and not p.dishonest else []

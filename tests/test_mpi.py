@@ -95,6 +95,19 @@ def test_mpiexec_count_mode_matches_canonical(name):
 
 
 @needs_mpi
+@pytest.mark.parametrize("name,owners", [("case011", 2), ("case013", 2), ("case011", 3), ("case013", 4)])
+def test_mpiexec_count_mode_sharded_owners(name, owners):
+    """The mpiexec GPU-owner branch at G > 1 (tfg.count_owners: owner
+    selection, the group id sent from rank 0 over MPI, ShardCounter over the
+    owners' shards of the injected lists) with the numpy engine and an MPI
+    all-reduce in place of RCCL: decisions equal the canonical fixtures."""
+    case = CASES[name]
+    assert case["n"] + 1 >= owners
+    got = _mpiexec(case["n"] + 1, [name, "--rounds", "epoch", "--mode", "count", "--owners", str(owners)])
+    _compare(got, case["canonical"], traffic=False)
+
+
+@needs_mpi
 @pytest.mark.parametrize("name", ["case009", "case010"])
 def test_mpiexec_reference_rounds_honest(name):
     """nDishonest = 0: the round loop never re-broadcasts, so the reference's

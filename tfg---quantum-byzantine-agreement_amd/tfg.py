@@ -66,6 +66,45 @@ def _outcome(res, verbose):
         print("Success:", res["success"])
 
 
+class RcclLink:
+    """How the GPU owners of an mpiexec count run form their all-reduce group:
+    an RCCL communicator through the C ABI (qba_rccl_init), its unique id
+    created on rank 0 and sent to the other owners over MPI."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        from .engine import Engine
+        return Engine.rccl_unique_id()
+
+    @staticmethod
+    def allreduce(eng, uid: bytes, owners: int, rank: int):
+        eng.rccl_init(uid, owners, rank)
+        return countmode.rccl_allreduce(eng)
+
+
+def count_owners(world, mpi, ndev: int, make_engine, link=RcclLink):
+    """Count mode under mpiexec: the first G = min(ranks,
+    GPUs) ranks own a GPU each (device = rank % ndev) and shard the count pass
+    (countmode.ShardCounter); for G > 1 rank 0 makes the group's unique id and
+    sends it to owners 1..G-1 over MPI, and every owner joins the group.
+    Returns (engine or None, CountParty keyword arguments).  make_engine and
+    link are the seams the CPU test of G > 1 owners fills with the numpy engine
+    and an all-reduce over MPI (tests/mpi_driver.py --owners)."""
+    rank, size = world.Get_rank(), world.Get_size()
+    g = min(size, ndev)
+    eng = make_engine(rank % ndev) if rank < g else None
+    kw = {}
+    if g > 1 and rank < g:
+        uid = np.frombuffer(link.unique_id() if rank == 0 else bytes(128), np.uint8).copy()
+        if rank == 0:
+            for r in range(1, g):
+                world.Send([uid, mpi.INT], dest=r, tag=RCCL_ID_TAG)
+        else:
+            world.Recv([uid, mpi.INT], source=0, tag=RCCL_ID_TAG)
+        kw["counter"] = countmode.ShardCounter(eng, rank, g, link.allreduce(eng, uid.tobytes(), g, rank))
+    return eng, kw
+
+
 def _mpiexec(a, mpi, size_l, verbose, log) -> int:
     import torch
     from .engine import Engine
@@ -84,17 +123,7 @@ def _mpiexec(a, mpi, size_l, verbose, log) -> int:
     comm = comm_mod.EpochComm(world) if a.rounds == "epoch" else world
     kw = {}
     if a.mode == "count":
-        g = min(size, ndev)
-        eng = Engine(rank % ndev) if rank < g else None
-        if g > 1 and rank < g:  # RCCL communicator of the GPU owners, id over MPI
-            uid = np.frombuffer(Engine.rccl_unique_id() if rank == 0 else bytes(128), np.uint8).copy()
-            if rank == 0:
-                for r in range(1, g):
-                    world.Send([uid, mpi.INT], dest=r, tag=RCCL_ID_TAG)
-            else:
-                world.Recv([uid, mpi.INT], source=0, tag=RCCL_ID_TAG)
-            eng.rccl_init(uid.tobytes(), g, rank)
-            kw["counter"] = countmode.ShardCounter(eng, rank, g, countmode.rccl_allreduce(eng))
+        eng, kw = count_owners(world, mpi, ndev, Engine, RcclLink)
         cls = countmode.CountParty
     else:
         eng = Engine(rank % ndev)
