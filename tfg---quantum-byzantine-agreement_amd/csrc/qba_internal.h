@@ -14,22 +14,12 @@
 #include "../../include/qba.h"
 
 // ---------------------------------------------------------------------------
-// Experiment switches (tools/exp/build.sh) exist only for A/B builds; several
-// make the results wrong by design.  A build that sets any of them must also
-// define QBA_EXPERIMENT_BUILD, so the shipped libqba.so cannot carry one, and
-// qba_build_flags() reports which were compiled in (0 for a shipped build;
-// tests/test_oracle_golden.py asserts it).
+// Experiment builds (tools/exp/build.sh, optionally with the attribution
+// probes of tools/exp/probes.patch) define QBA_EXPERIMENT_BUILD; several make
+// the results wrong by design.  qba_build_flags() reports it (0 for a shipped
+// build; tests/test_oracle_golden.py asserts it).
 // ---------------------------------------------------------------------------
-#if defined(QBA_EXP_LDSPAD) || defined(QBA_EXP_NOCOUNT) || defined(QBA_EXP_NOSEEN) || defined(QBA_EXP_NOSTORE) ||   \
-    defined(QBA_EXP_CHEAPRNG) || defined(QBA_EXP_PADVALU) || defined(QBA_EXP_PADLDS) || defined(QBA_EXP_NOATOMIC) || \
-    defined(QBA_EXP_SKIP) || defined(QBA_EXP_TIMING) || defined(QBA_EXP_GRID) ||          \
-    defined(QBA_WIDE_QPT) || defined(QBA_MINW) || defined(QBA_QTAB_MASK) || defined(QBA_RED_ROWS) ||                \
-    defined(QBA_RED_ALL_IN_FLIGHT) || defined(QBA_QUEUE) || defined(QBA_PAIRWISE) || defined(QBA_SGPR_LEAN) ||      \
-    defined(QBA_QUAD_RANGE) || defined(QBA_NT_STORE) || defined(QBA_LBLOCK) || defined(QBA_DBLOCK) ||               \
-    defined(QBA_GRID_QPT) || defined(QBA_ZERO_AT_END) || defined(QBA_ONLY_N) || defined(QBA_PAIRBINS) || defined(QBA_SAMP_TRIM) || defined(QBA_SPLIT_LAST) || defined(QBA_RANK_MASK) || defined(QBA_PUSH_W2) || defined(QBA_PB_ALIGN) || defined(QBA_DEF_PAIRWISE) || defined(QBA_PB_DRAIN_PRIO) || defined(QBA_DEF_GTAB) || defined(QBA_DEF_WAVES)
-#ifndef QBA_EXPERIMENT_BUILD
-#error "an experiment switch is set without QBA_EXPERIMENT_BUILD (tools/exp/build.sh): not a shippable libqba"
-#endif
+#ifdef QBA_EXPERIMENT_BUILD
 #define QBA_BUILD_EXPERIMENT_FLAGS 1
 #else
 #define QBA_BUILD_EXPERIMENT_FLAGS 0
@@ -38,15 +28,8 @@
 #define QBA_MAX_FACTORS 16
 #define QBA_MAX_TABLE 4096   // uint64 table entries per kind (LDS budget)
 #define QBA_BLOCK 256        // threads per workgroup (batched / helper kernels)
-#ifndef QBA_SGPR_LEAN  // list kernels: round keys / row bases re-derived on the scalar unit
-#define QBA_SGPR_LEAN 1
-#endif
-#ifndef QBA_LBLOCK
 #define QBA_LBLOCK 1024      // threads per workgroup of the streaming list kernels (2 per CU at n = 11)
-#endif
-#ifndef QBA_DBLOCK
 #define QBA_DBLOCK 768       // ... of the deferred-reduction list kernel (small launches)
-#endif
 #define QBA_CHUNK (1ull << 31)  // entries per list-kernel launch (32-bit offsets, u32 bins)
 #define QBA_EPT 4            // entries per thread per step: one dword per list row
 
@@ -63,15 +46,11 @@ __device__ __forceinline__ uint32_t qba_xor3(uint32_t a, uint32_t b, uint32_t k)
 }
 
 // Keys are wave-uniform (kernel arguments or block-uniform): they stay in SGPRs.
-// SK (QBA_SGPR_LEAN callers with wave-uniform keys): round keys re-derived per
+// SK (list-kernel callers with wave-uniform keys): round keys re-derived per
 // block on the scalar unit.
 template <bool SK = false>
 __device__ __forceinline__ QbaU4 qba_philox_k(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1) {
-#ifdef QBA_EXP_CHEAPRNG  // experiment builds only (tools/exp): cost of the generator
-  const uint32_t h = (c0 ^ k0) * 0x9E3779B9u + c1 + c2 * 0x85EBCA6Bu;
-  return QbaU4{h, h * 0xC2B2AE35u, h ^ (h >> 15) ^ k1, (h * 0x27D4EB2Fu) ^ c3};
-#endif
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;

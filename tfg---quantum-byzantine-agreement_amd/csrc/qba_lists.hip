@@ -436,14 +436,3 @@ extern "C" int qba_philox_dev(qba_ctx *ctx, const uint32_t *ctr, int64_t n, uint
   QBA_HIP(hipGetLastError());
   return QBA_OK;
 }
-
-#ifdef QBA_EXP_TIMING
-// experiment builds: the phase timestamps of the last counting launch
-// (8 x u64 per workgroup after its slab rows; see qba_k_lists)
-extern "C" QBA_API int qba_exp_timing(qba_ctx *ctx, int n, int grid, uint64_t *host) {
-  QBA_HIP(hipDeviceSynchronize());
-  const char *src = reinterpret_cast<const char *>(ctx->slab) + (size_t)grid * nbins_of(n) * sizeof(uint32_t);
-  QBA_HIP(hipMemcpy(host, src, (size_t)grid * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  return QBA_OK;
-}
-#endif

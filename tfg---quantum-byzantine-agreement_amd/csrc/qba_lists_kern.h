@@ -18,43 +18,14 @@
 
 #include "qba_lists.h"
 
-#ifndef QBA_WIDE_QPT  // quads per thread-step of the wide kernels (experiment builds: 4)
-#define QBA_WIDE_QPT 2
-#endif
-#ifndef QBA_QUEUE  // count Q entries 64 at a time from a per-wave LDS queue
-#define QBA_QUEUE 1
-#endif
-#ifndef QBA_QUAD_RANGE  // count: one range test per quad of entries (experiment builds: 0)
-#define QBA_QUAD_RANGE 1
-#endif
-#ifndef QBA_QTAB_MASK  // stage-table reads by the Q-correlated lanes only (experiment)
-#define QBA_QTAB_MASK 0
-#endif
-#ifndef QBA_PAIRWISE  // closed sampler: a quad's two pairs one after the other (fewer live VGPRs)
-#define QBA_PAIRWISE 1
-#endif
-#ifndef QBA_DEF_PAIRWISE  // ... in the deferred (configs[1]) kernel: interleaved, more ILP at low occupancy
-#define QBA_DEF_PAIRWISE 0
-#endif
-#ifndef QBA_DEF_WAVES  // deferred kernel: waves per SIMD it is compiled for
-#define QBA_DEF_WAVES 6
-#endif
-#ifndef QBA_NT_STORE  // nontemporal list stores (experiment builds: 0)
-#define QBA_NT_STORE 1
-#endif
-#ifndef QBA_SAMP_TRIM  // closed sampler: rank fallback in its rare branch, no redundant mask / OR
-#define QBA_SAMP_TRIM 1
-#endif
-#ifndef QBA_PB_ALIGN  // pair bins: array A 1-KiB aligned, base = one v_and_or
-#define QBA_PB_ALIGN 1
-#endif
-#ifndef QBA_PB_DRAIN_PRIO  // pair-bin drains at raised wave priority
-#define QBA_PB_DRAIN_PRIO 1
-#endif
-#ifndef QBA_RANK_MASK  // not-Q entries read table entry 0 (LDS broadcast) instead of a random one
-#define QBA_RANK_MASK 1
-#endif
-
+// Measured shapes of the list kernels (the rejected
+// alternatives and the attribution probes live in tools/exp/probes.patch)
+constexpr int QBA_WIDE_QPT = 2;      // quads per thread-step of the wide kernels (one 8-B / 4-B row vector)
+constexpr int QBA_PAIRWISE = 1;      // closed sampler: a quad's two pairs one after the other (fewer live VGPRs)
+constexpr int QBA_DEF_PAIRWISE = 0;  // ... in the deferred (configs[1]) kernel: interleaved, more ILP at 6 waves
+constexpr int QBA_DEF_WAVES = 6;     // deferred kernel: waves per SIMD it is compiled for
+constexpr int QBA_GRID_QPT = 2;      // quads per thread the grid is sized for
+constexpr int QBA_RED_ROWS = 32;     // slab rows per reduce workgroup
 
 template <int NP>
 struct QCfg {
@@ -289,57 +260,80 @@ struct QbaClosed {
   uint32_t rank, w0;
 };
 
+// Philox4x32-10 on the scalar unit: the same function as qba_philox for
+// wave-uniform arguments, in plain XORs (v_bitop3 has no scalar form)
+__device__ __forceinline__ QbaU4 qba_philox_s(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                              uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return QbaU4{c0, c1, c2, c3};
+}
+
+// The rank of an entry whose two Lemire tests failed: the first accepted word
+// of philox(ctr = {p_lo, p_hi, 0x80000000 + t, h}), t = 1, 2, ... (arguments
+// wave-uniform: scalar unit)
+template <int NP>
+__device__ __forceinline__ uint32_t qba_rank_retry_s(uint32_t plo, uint32_t phi, uint32_t h, uint32_t k0, uint32_t k1) {
+  for (uint32_t t = 1;; ++t) {
+    const QbaU4 y = qba_philox_s(plo, phi, 0x80000000u + t, h, k0, k1);
+    if (qba_accept<NP>(y.x, CF<NP>::T32)) return y.x;
+    if (qba_accept<NP>(y.y, CF<NP>::T32)) return y.y;
+    if (qba_accept<NP>(y.z, CF<NP>::T32)) return y.z;
+    if (qba_accept<NP>(y.w, CF<NP>::T32)) return y.w;
+  }
+}
+
 template <int NP>
 __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
                                                 uint32_t k0, uint32_t k1, QbaClosed &c) {
   using F = CF<NP>;
   // group g >= 1 = nibble g of (w1 low nibbles, w1 high nibbles, w0 high
   // nibbles) in byte order, group 0 = group 1: the masked words ARE the byte
-  // layout, one v_perm in all (w0's low nibbles carry isQ and r)
-#if QBA_SAMP_TRIM
-  // unmasked: qba_closed_finish masks every not-Q word with ~qm & M4 anyway
+  // layout, one v_perm in all (w0's low nibbles carry isQ and r); unmasked:
+  // qba_closed_finish masks every not-Q word with ~qm & M4 anyway
   c.nqr[0] = qba_perm_b(w1, w1, 0x03020101u);
-#else
-  const uint32_t a = w1 & F::M4;
-  c.nqr[0] = qba_perm_b(a, a, 0x03020101u);
-#endif
   c.nqr[1] = w1 >> 4;
   c.nqr[2] = w0 >> 4;
   c.nqr[3] = 0u;
   c.w0 = w0;
-#if QBA_SAMP_TRIM
   // w1 is the rank word unless its Lemire test fails (P = (2^32 mod n!) /
   // 2^32, 0.56 % at n = 11): the fallback words are chosen inside the rare
   // branch, not by a select on every entry
   uint32_t rank = w1;
+  bool retry = false;
   if (__builtin_expect(!qba_accept<NP>(w1, F::T32), 0)) {
     rank = w0 & ~31u;
-    if (!qba_accept<NP>(rank, F::T27)) {  // ~(T32 T27) / 2^59 per entry
-#else
-  const bool o1 = qba_accept<NP>(w1, F::T32);
-  uint32_t rank = o1 ? w1 : (w0 & ~31u);
-  if (__builtin_expect(!o1 && !qba_accept<NP>(rank, F::T27), 0)) {  // ~(T32 T27) / 2^59 per entry
-  {
-#endif
-    bool ok = false;
-    for (uint32_t t = 1; !ok; ++t) {
-      const QbaU4 y = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0x80000000u + t, h, k0, k1);
-      const uint32_t cand[4] = {y.x, y.y, y.z, y.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (!ok && qba_accept<NP>(cand[i], F::T32)) {
-          ok = true;
-          rank = cand[i];
-        }
-    }
+    // both tests failed (P = 6e-4 per entry at n = 11); a not-Q entry's rank
+    // is discarded, so only Q-correlated entries retry
+    retry = !qba_accept<NP>(rank, F::T27) && (w0 & 1u);
   }
+  // The retries of the wave, lane by lane on the SCALAR unit: no VGPR is
+  // needed, so nothing is spilled.  (Inline, the retry loop pushed the
+  // kernel past its 64 VGPRs: a scratch reload in the loop made the compiler
+  // wait for every outstanding row store -- s_waitcnt vmcnt(0) -- before the
+  // first Philox round of every step.)
+  for (uint64_t m = __ballot(retry); m; m &= m - 1) {  // wave-uniform
+    const int l = __builtin_ctzll(m);
+    const uint32_t r = qba_rank_retry_s<NP>(__builtin_amdgcn_readlane((uint32_t)p, l),
+                                            __builtin_amdgcn_readlane((uint32_t)(p >> 32), l),
+                                            __builtin_amdgcn_readlane(h, l), k0, k1);
+    if ((int)__lane_id() == l) rank = r;
   }
   // a not-Q entry discards its table words (qba_closed_finish selects its
   // nibbles): rank 0 sends its three reads to one address per table, served
   // as an LDS broadcast, so only the Q lanes' random reads meet bank conflicts
-#if QBA_RANK_MASK
   rank &= (uint32_t)__builtin_amdgcn_sbfe((int)w0, 0, 1);
-#endif
   c.rank = rank;
 }
 
@@ -347,22 +341,18 @@ template <int NP>
 __device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint4 &A, const uint2 &sB,
                                                   uint32_t sC, uint32_t (&D)[CF<NP>::ND]) {
   using F = CF<NP>;
-#if QBA_SAMP_TRIM
   // A.w (zero in the table) is kept alive by an empty asm, so the read stays
   // one ds_read_b128 (4 LDS cycles, a ds_read_b96 takes 8) without an OR
   uint32_t q[4] = {A.x, A.y, A.z, A.w};
   asm volatile("" ::"v"(A.w));
-#else
-  // A.w is zero in the table; folding it in keeps the read one ds_read_b128
-  // (4 LDS cycles) instead of a ds_read_b96 (8).
-  uint32_t q[4] = {A.x | A.w, A.y, A.z, A.w};
-#endif
   const uint32_t y0 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.x);
   uint32_t y1 = qba_perm_b(q[F::WIN + 1], q[F::WIN], sB.y);
   if constexpr (F::RC > 1) y1 = qba_perm_b(y1, y0, sC);  // stage C moves window bytes 4..7 only
   q[F::WIN] = y0;
   q[F::WIN + 1] = y1;
-  const uint32_t R = ((c.w0 >> 1) & (uint32_t)(QCfg<NP>::W - 1)) * 0x01010101u;
+  // r in every byte: one v_perm (byte 0 to all four) instead of a quarter-rate
+  // v_mul_lo_u32 by 0x01010101
+  const uint32_t R = qba_perm_b(0u, (c.w0 >> 1) & (uint32_t)(QCfg<NP>::W - 1), 0u);
   // all ones for a Q-correlated entry: one v_bfe_i32, opaque so that each
   // word's select stays one v_bitop3 (qm ? q ^ R : nq) instead of and + cmp
   // for a mask plus a v_cndmask per word
@@ -510,9 +500,6 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
   using F = CF<NP>;
   const uint32_t l0 = D[0] & 0xffu, l1 = (D[0] >> 8) & 0xffu;
   if (!known_q && l0 == l1) return;  // the Q-entry queue holds only entries with L0 != L1
-#ifdef QBA_EXP_NOCOUNT
-  if (l0 != 0xfffu) return;
-#endif
   uint32_t bad = 0;
 #pragma unroll
   for (int i = 0; i < F::ND; ++i) {
@@ -545,11 +532,7 @@ __device__ __forceinline__ void qba_count_d(const uint32_t (&D)[CF<NP>::ND], uin
       const int g = 4 * i + b;
       if (g < C::G && g != 1) {  // H[u][1][x] = [x == u] |P_u|, derived when reduced
         const uint32_t a = qba_add_byte(hb, E, b);
-#ifdef QBA_EXP_NOATOMIC  // experiment builds: the address work without the LDS atomic
-        asm volatile("" ::"v"(a));
-#else
         atomicAdd((uint32_t *)((qba_lds_u32 *)(uintptr_t)a + g * C::WP), 1u);
-#endif
       }
     }
   }
@@ -619,7 +602,7 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
       for (int jp = 0; jp < 2; ++jp) {
         QbaClosed cl[2];
         const uint64_t p = ((uint64_t)phi << 32) | (uint64_t)(plo + (uint32_t)jp);
-        const QbaU4 x = qba_philox_k<QBA_SGPR_LEAN != 0>(plo + (uint32_t)jp, phi, 0u, 0u, k0, k1);
+        const QbaU4 x = qba_philox_k<true>(plo + (uint32_t)jp, phi, 0u, 0u, k0, k1);
         qba_closed_rank<NP>(x.x, x.y, p, 0u, k0, k1, cl[0]);
         qba_closed_rank<NP>(x.z, x.w, p, 1u, k0, k1, cl[1]);
         uint4 A[2];
@@ -650,21 +633,8 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
       uint4 A[4];
       uint2 sB[4];
       uint32_t sC[4];
-#if QBA_QTAB_MASK
-      // only Q-correlated lanes read the stage tables: half the lanes of each
-      // LDS read, so fewer bank conflicts (the not-Q lanes' values are
-      // discarded by qba_closed_finish's select)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        A[j] = make_uint4(0u, 0u, 0u, 0u);
-        sB[j] = make_uint2(0u, 0u);
-        sC[j] = 0u;
-        if (cl[j].w0 & 1u) qba_closed_tables<NP>(cl[j].rank, pl, A[j], sB[j], sC[j]);
-      }
-#else
 #pragma unroll
       for (int j = 0; j < 4; ++j) qba_closed_tables<NP>(cl[j].rank, pl, A[j], sB[j], sC[j]);
-#endif
 #pragma unroll
       for (int j = 0; j < 4; ++j) qba_closed_finish<NP>(cl[j], A[j], sB[j], sC[j], D[j]);
       return;
@@ -697,7 +667,7 @@ template <int NP>
 __device__ __forceinline__ void qba_count_quad(const uint32_t (&D)[4][CF<NP>::ND], int valid,
                                                uint32_t *hist, const uint32_t *row) {
   const uint32_t one = 0x00010001u;
-  if (QBA_QUAD_RANGE && qba_rows_in_range<NP>(row)) {
+  if (qba_rows_in_range<NP>(row)) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (j < valid) qba_count_d<NP>(D[j], one, hist, true);
@@ -709,7 +679,7 @@ __device__ __forceinline__ void qba_count_quad(const uint32_t (&D)[4][CF<NP>::ND
 }
 
 // ---------------------------------------------------------------------------
-// Wave-level Q-entry queue (QBA_QUEUE): only Q entries are counted, so with
+// Wave-level Q-entry queue: only Q entries are counted, so with
 // per-entry counting half the lanes of every count instruction idle.  Each
 // wave appends its Q entries (byte-layout words, SoA in LDS) to a ring of
 // QBA_QCAP slots and counts them 64 at a time with every lane busy.  All
@@ -821,9 +791,6 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
 // for sampled lists a wrap needs a bin ~18 sigma above its mean and never
 // happens in practice (tests force it with QBA_LIST_GRID).
 // ---------------------------------------------------------------------------
-#ifndef QBA_PAIRBINS
-#define QBA_PAIRBINS 1
-#endif
 #define QBA_PB_BUDGET (1u << 18)  // entries per workgroup per launch (wrap-free in practice)
 struct QbaPB {
   static constexpr int WORDS = 8192;       // A [4096] then B [4096]
@@ -837,7 +804,7 @@ struct QbaPB {
 template <int NP, int MODE, int SAMP, int PK>
 struct QbaUsePB {
   static constexpr bool value =
-      QBA_PAIRBINS && NP == 11 && ((MODE == 1 && SAMP == QBA_S_CLOSED) || (MODE == 2 && PK == 1));
+      NP == 11 && ((MODE == 1 && SAMP == QBA_S_CLOSED) || (MODE == 2 && PK == 1));
 };
 
 // base + 16-bit half h of x in one VALU op (v_add_u32 with an SDWA word select)
@@ -851,11 +818,7 @@ __device__ __forceinline__ uint32_t qba_add_word(uint32_t base, uint32_t x, int 
 }
 
 __device__ __forceinline__ void qba_lds_add(uint32_t addr, uint32_t v) {
-#ifdef QBA_EXP_NOATOMIC  // experiment builds: the address work without the LDS atomic
-  asm volatile("" ::"v"(addr), "v"(v));
-#else
   atomicAdd((uint32_t *)qba_lds(addr), v);
-#endif
 }
 
 // Count one Q-correlated entry (c0, c1) into the pair bins; hA = LDS byte
@@ -868,22 +831,15 @@ __device__ __forceinline__ void qba_count_pb(uint32_t c0, uint32_t c1, uint32_t 
   const uint32_t t = c0 >> 2;
   const uint32_t E1 = t & 0x3c3c3c3cu;          // groups 4-7, x4
   const uint32_t E2 = c1 << 2;                  // groups 8-11, x4
-#if QBA_PB_ALIGN
   // A + 64 u: u = group 1 sits at bits 6-9 of c0 >> 2, and A is 1-KiB
   // aligned (qba_lists_body), so the base is one v_and_or
   const uint32_t hb = (t & 0x3c0u) | hA;
-#else
-  const uint32_t hb = (__builtin_amdgcn_ubfe(c0, 8, 4) << 6) + hA;  // A + 64 u
-#endif
   qba_lds_add(qba_add_word(hb, E0, 0) + B, 0x100u);      // group 0 at (x_0, u, u), B lanes 1-3
   qba_lds_add(qba_add_word(hb, E0, 1), 0x1u);            // (2,3)   A lane 0
   qba_lds_add(qba_add_word(hb, E1, 0), 0x100u);          // (4,5)   A lane 1
   qba_lds_add(qba_add_word(hb, E1, 1), 0x10000u);        // (6,7)   A lane 2
   qba_lds_add(qba_add_word(hb, E2, 0), 0x1000000u);      // (8,9)   A lane 3
   qba_lds_add(qba_add_word(hb, E2, 1) + B, 0x1u);        // (10,11) B lane 0
-#ifdef QBA_EXP_NOCOND3  // experiment builds: the test below skipped (A/B of its cost; results wrong on collisions)
-  return;
-#endif
   // Cond3 (tfg.py:96-98) on every counted entry: its 12 values are pairwise
   // distinct iff the union of their 16-bit one-hots has 12 bits.  Each
   // v_pk_lshlrev_b16 makes two one-hots from the low nibbles of the two
@@ -928,13 +884,9 @@ __device__ __forceinline__ void qba_q_drain_pb(QbaWaveQ &q, uint32_t nv) {
   typedef uint32_t v2u __attribute__((ext_vector_type(2)));
   const v2u c = *reinterpret_cast<__attribute__((address_space(3))) v2u *>(
       static_cast<uintptr_t>(qba_qpb_addr(q, q.tail + lane)));
-#if QBA_PB_DRAIN_PRIO
   __builtin_amdgcn_s_setprio(2);  // as qba_q_drain
-#endif
   if (nv >= 64 || lane < nv) qba_count_pb<NP>(c.x, c.y, q.hoff);
-#if QBA_PB_DRAIN_PRIO
   __builtin_amdgcn_s_setprio(0);
-#endif
   q.tail += nv;
   q.qn -= nv;
 }
@@ -1055,30 +1007,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
         }
       }
     }
-#ifdef QBA_EXP_PADVALU  // experiment builds: probe VALU headroom (independent xor chains)
-    {
-      uint32_t z0 = row[0][0], z1 = row[0][1], z2 = row[0][2], z3 = row[0][3];
-      for (int i = 0; i < QBA_EXP_PADVALU / 4; ++i) {
-        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z0) : "v"(row[0][4]));
-        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z1) : "v"(row[0][5]));
-        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z2) : "v"(row[0][6]));
-        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z3) : "v"(row[0][7]));
-      }
-      asm volatile("" ::"v"(z0), "v"(z1), "v"(z2), "v"(z3));
-    }
-#endif
-#ifdef QBA_EXP_PADLDS  // experiment builds: probe LDS headroom (broadcast reads, consumed)
-    {
-      uint32_t z = 0;
-      for (int i = 0; i < QBA_EXP_PADLDS; ++i) z ^= reinterpret_cast<volatile uint32_t *>(hist)[4 * i];
-      asm volatile("" ::"v"(z));
-    }
-#endif
-#ifdef QBA_EXP_NOSTORE
-    if (row[0][0] == 0x12345678u && row[0][1] == 0x9abcdef0u)
-#else
     if (!TAIL && act)
-#endif
     {
 #pragma unroll
       for (int g = 0; g < C::G; ++g) {
@@ -1094,13 +1023,9 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
         asm("" : "+s"(rb));
         typedef __attribute__((address_space(1))) V GV;  // global, not flat
         GV *dst = reinterpret_cast<GV *>(rb + c0);
-#if QBA_NT_STORE
         // the rows are streamed out once: nontemporal stores move the 12 rows of
         // 1.25e8 entries in 0.313 ms instead of 0.356 (tools/ubench/stores2)
         __builtin_nontemporal_store(v, dst);
-#else
-        *dst = v;
-#endif
       }
     } else if (TAIL) {
       for (int g = 0; g < C::G; ++g)
@@ -1210,12 +1135,8 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
         }
       }
     }
-#ifdef QBA_EXP_NOSTORE  // experiment builds: the row stores and their transposes skipped (never true)
-    if (Dp[0][0] == 0x12345678u && Dp[1][1] == 0x9abcdef0u) {
-#else
     if (!TAIL && act) {
-#endif
-      uint64_t rbl = 0;  // QBA_SGPR_LEAN: the running row base
+      uint64_t rbl = 0;  // the running row base
       (void)rbl;
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
@@ -1229,7 +1150,6 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
           const int g = 4 * i + gg;
           if (g >= C::G) continue;
           // row base opaque in SGPRs, 32-bit lane offset (as qba_step)
-#if QBA_SGPR_LEAN
           // one running row pointer (s_add_u32 / s_addc_u32 per row) instead
           // of n+1 loop-invariant 64-bit bases
           if (g == 0) {
@@ -1240,16 +1160,8 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
             asm volatile("" : "+s"(rbl));
           }
           const uint64_t rb = rbl;
-#else
-          uint64_t rb = reinterpret_cast<uint64_t>(lists) + (uint64_t)g * ld;
-          asm("" : "+s"(rb));
-#endif
           if constexpr (QPT == 2) {
-#if QBA_NT_STORE
             __builtin_nontemporal_store(r[gg], reinterpret_cast<GU *>(rb + cb));
-#else
-            *reinterpret_cast<GU *>(rb + cb) = r[gg];
-#endif
           } else if (!((reinterpret_cast<uintptr_t>(lists) | ld) & 1)) {  // uniform: rows 2-byte aligned (cb is even)
             typedef __attribute__((address_space(1))) uint16_t GH;
             *reinterpret_cast<GH *>(rb + cb) = (uint16_t)r[gg];
@@ -1323,9 +1235,6 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   return hist;
 }
 
-#ifndef QBA_ZERO_AT_END
-#define QBA_ZERO_AT_END 1
-#endif
 // The outputs of a counting launch start at zero unless the call accumulates:
 // the list kernel's workgroup 0 clears them before the reduction adds in.
 struct QbaZero {
@@ -1430,12 +1339,8 @@ __device__ __forceinline__ bool qba_pb_flush(uint32_t *hist, uint32_t *row) {
 // latency of the histogram atomics: -3 % cycles per launch against 6 waves
 // of 768 threads (profiles/r3/r3k).  The table samplers (n > 11) need more
 // registers and keep the compiler's choice.
-#ifdef QBA_MINW  // experiment builds: minimum waves per SIMD (caps the VGPRs)
-#define QBA_LISTS_BOUNDS __launch_bounds__(QBA_LBLOCK, QBA_MINW)
-#else
 #define QBA_LISTS_BOUNDS \
   __attribute__((amdgpu_flat_work_group_size(1, QBA_LBLOCK), amdgpu_waves_per_eu(SAMP == QBA_S_CLOSED ? 8 : 1)))
-#endif
 #define QBA_LISTS_BOUNDS_PB \
   __attribute__((amdgpu_flat_work_group_size(1, QBA_LBLOCK), amdgpu_waves_per_eu(8)))
 // PK = 1: nibble rows (qba_step_pk), ld in bytes of packed row.
@@ -1454,36 +1359,23 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   const uint32_t bid = blockIdx.x - red, nblk = gridDim.x - red - tail;
   const uint64_t *pat, *apat, *thr;
   const uint32_t *pl;
-#ifdef QBA_EXP_TIMING  // experiment builds: per-workgroup phase timestamps after the slab rows
-  uint64_t *tsl = reinterpret_cast<uint64_t *>(slab + (size_t)nblk * C::NBP) + 8 * bid;
-  const uint64_t ts0 = wall_clock64();
-#endif
   uint32_t *hist = qba_stage<NP, MODE, SAMP, BS>(ps, lds, pat, apat, thr, pl);
-  if constexpr (CNT && QBA_PB_ALIGN) {  // pair bins: array A 1-KiB aligned (qba_count_pb ORs 64 u into its address)
+  if constexpr (CNT) {  // pair bins: array A 1-KiB aligned (qba_count_pb ORs 64 u into its address)
     const uint32_t h = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     hist += (((h + 1023u) & ~1023u) - h) / 4;
   }
   if (MODE != 0) {
     constexpr int NZ = CNT ? QbaPB::AREA : C::NBP;
     for (int i = threadIdx.x; i < NZ; i += BS) hist[i] = 0u;
-#if !QBA_ZERO_AT_END
-    if (bid == 0) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
-#endif
   }
   __syncthreads();
-#ifdef QBA_EXP_TIMING
-  const uint64_t ts1 = wall_clock64();
-#endif
-#ifndef QBA_EXP_SKIP  // experiment builds only: 1 = no main loop / tail, 2 = no slab flush
-#define QBA_EXP_SKIP 0
-#endif
-  const uint32_t nunits = (QBA_EXP_SKIP & 1) ? 0u : count / (4 * QPT);
+  const uint32_t nunits = count / (4 * QPT);
   // the grid stride in an SGPR, read once: reloading gridDim in the loop is a
   // scalar load whose s_waitcnt lgkmcnt(0) also drains every LDS atomic the
   // wave has in flight (-2% step time)
   const uint32_t ustride = __builtin_amdgcn_readfirstlane(nblk * BS);
   const uint32_t u0 = bid * BS + threadIdx.x;
-  if constexpr (MODE != 0 && QBA_QUEUE) {
+  if constexpr (MODE != 0) {
     QbaWaveQ wq;
     if constexpr (CNT) {  // 8-B slots after the pair bins, each ring aligned to its size
       const uint32_t h = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist + QbaPB::AREA * 4;
@@ -1515,7 +1407,7 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   }
   // the remaining < 4 QPT entries: whole quads, then the partial one
   const uint32_t r0 = nunits * (4 * QPT), rq = (count - r0 + 3) >> 2;
-  if (!(QBA_EXP_SKIP & 1) && bid == nblk - 1 && threadIdx.x < rq) {
+  if (bid == nblk - 1 && threadIdx.x < rq) {
     const uint32_t c0 = r0 + 4 * threadIdx.x;
     if (c0 + 4 <= count)
       qba_step_l<NP, MODE, SAMP, 1, false, PK, false, CNT, PW>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
@@ -1524,13 +1416,10 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   }
   if (MODE != 0) {
     __syncthreads();
-#ifdef QBA_EXP_TIMING
-    const uint64_t ts2 = wall_clock64();
-#endif
     uint32_t *row = slab + (size_t)bid * C::NBP;
     bool classic = !CNT;
     if constexpr (CNT) {
-      if (!(QBA_EXP_SKIP & 2) && qba_pb_flush<NP, BS>(hist, row)) {
+      if (qba_pb_flush<NP, BS>(hist, row)) {
         // a pair-bin lane wrapped (never for sampled lists at QBA_PB_BUDGET
         // entries per workgroup): recount this workgroup's entries -- the
         // same units and tail as above -- from the rows it stored, into the
@@ -1556,26 +1445,14 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
         classic = true;
       }
     }
-    if (classic && !(QBA_EXP_SKIP & 2)) {
+    if (classic) {
       uint4 *dst = reinterpret_cast<uint4 *>(row);
       const uint4 *src = reinterpret_cast<const uint4 *>(hist);
       for (int i = threadIdx.x; i < C::NBP / 4; i += BS) dst[i] = src[i];
     }
-#ifdef QBA_EXP_TIMING
-    if (threadIdx.x == 0) {
-      tsl[0] = ts0;
-      tsl[1] = ts1;
-      tsl[2] = ts2;
-      tsl[3] = wall_clock64();
-      tsl[4] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));   // HW_ID: CU / SH / SE
-      tsl[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((32 - 1) << 11));  // XCC_ID
-    }
-#endif
-#if QBA_ZERO_AT_END
     // any point of this kernel precedes the reduction; at the end it leaves
     // the main loop's code placement alone
     if (bid == nblk - 1) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
-#endif
   }
 }
 
@@ -1780,7 +1657,6 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     // QPT quads per thread-step, Q entries counted 64 at a time from the
     // per-wave LDS queue (as qba_k_lists), then the < 4 QPT remaining entries
     const uint32_t nunits = (uint32_t)count / (4 * QPT);
-#if QBA_QUEUE
     QbaWaveQ wq;
     wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
@@ -1794,11 +1670,6 @@ __global__ void __launch_bounds__(QBA_BLOCK)
                                               L, ld, hist, &wq, act);
     }
     while (wq.qn) qba_q_drain<NP, true>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
-#else
-    for (uint32_t u = threadIdx.x; u < nunits; u += QBA_BLOCK)
-      qba_step_l<NP, 1, SAMP, QPT, false, PK>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld,
-                                        hist);
-#endif
     const uint32_t r0 = nunits * (4 * QPT), rq = ((uint32_t)count - r0 + 3) >> 2;
     if (threadIdx.x < rq) {
       const uint32_t c0 = r0 + 4 * threadIdx.x;
@@ -1832,12 +1703,6 @@ __global__ void __launch_bounds__(QBA_BLOCK)
 // qba_psize); the stats bins to the stats.  The list kernel of the same
 // launch zeroed the outputs unless the call accumulates, so no finalize pass
 // or accumulator is needed.
-#ifndef QBA_RED_ROWS  // slab rows per reduce workgroup
-#define QBA_RED_ROWS 32
-#endif
-#ifndef QBA_RED_ALL_IN_FLIGHT
-#define QBA_RED_ALL_IN_FLIGHT 0
-#endif
 template <int NP>
 __global__ void __launch_bounds__(256)
     qba_k_reduce(const uint32_t *__restrict__ slab, int nrows, int64_t *__restrict__ H,
@@ -1852,23 +1717,6 @@ __global__ void __launch_bounds__(256)
     const int b0 = blockIdx.y * QBA_RED_ROWS;
     const int b1 = b0 + QBA_RED_ROWS < nrows ? b0 + QBA_RED_ROWS : nrows;
     u64 s[4] = {0ull, 0ull, 0ull, 0ull};
-#if QBA_RED_ALL_IN_FLIGHT
-    // every row's load issued before the first is summed: one memory round
-    // trip per workgroup instead of RED_ROWS / 8 (the slab was just written by
-    // the list kernel and is read from beyond L2)
-    uint4 v[QBA_RED_ROWS];
-#pragma unroll
-    for (int r = 0; r < QBA_RED_ROWS; ++r)
-      v[r] = b0 + r < b1 ? reinterpret_cast<const uint4 *>(slab + (size_t)(b0 + r) * C::NBP)[q]
-                         : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int r = 0; r < QBA_RED_ROWS; ++r) {
-      s[0] += v[r].x;
-      s[1] += v[r].y;
-      s[2] += v[r].z;
-      s[3] += v[r].w;
-    }
-#else
 #pragma unroll 8
     for (int b = b0; b < b1; ++b) {
       const uint4 v = reinterpret_cast<const uint4 *>(slab + (size_t)b * C::NBP)[q];
@@ -1877,7 +1725,6 @@ __global__ void __launch_bounds__(256)
       s[2] += v.z;
       s[3] += v.w;
     }
-#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (!s[j]) continue;
@@ -1915,9 +1762,6 @@ __global__ void __launch_bounds__(256)
 
 // Persistent grid: every resident workgroup slot of the chip (LDS- and
 // register-limited occupancy), fewer when the launch has less work.
-#ifndef QBA_GRID_QPT
-#define QBA_GRID_QPT 2
-#endif
 static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count, int qpt = QBA_GRID_QPT,
                     int *cap_out = nullptr, int bs = QBA_LBLOCK) {
   // the occupancy query costs tens of microseconds: cached per (kernel, LDS)
@@ -1943,9 +1787,6 @@ static int grid_for(qba_ctx *ctx, const void *kern, size_t lds, uint64_t count, 
   // 1e6 entries) spreads over 163 workgroups instead of 82
   uint64_t g = (nquad + (uint64_t)qpt * bs - 1) / ((uint64_t)qpt * bs);
   const uint64_t cap = (uint64_t)ctx->num_cus * (uint64_t)per_cu;
-#ifdef QBA_EXP_GRID  // experiment builds: grid from the environment (QBA_EXP_GRID=<workgroups>)
-  if (const char *e = getenv("QBA_EXP_GRID")) g = strtoull(e, nullptr, 10);
-#endif
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   if (cap_out) *cap_out = (int)cap;
@@ -2009,11 +1850,8 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     lds += 1024 + (size_t)QbaPB::AREA * sizeof(uint32_t) + (size_t)(QBA_LBLOCK / 64 + 1) * QBA_QCAP * QbaPB::QSLOT;
   } else if (L.mode != 0) {
     lds += (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
-    if (QBA_QUEUE) lds += (size_t)(QBA_LBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
+    lds += (size_t)(QBA_LBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
   }
-#ifdef QBA_EXP_LDSPAD  // experiment builds: pad the launch's LDS (occupancy probe: one workgroup per CU)
-  if (L.mode == 1) lds += QBA_EXP_LDSPAD;
-#endif
   lds = (lds + 15) & ~(size_t)15;
   if (lds == 0) lds = 16;
   // 4*QPT-byte row vectors (QPT quads per thread-step) when the rows allow it
@@ -2120,7 +1958,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   } else if (kd) {
     dlds = table_lds<NP>(hs, samp) +
            (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
-    if (QBA_QUEUE) dlds += (size_t)(QBA_DBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
+    dlds += (size_t)(QBA_DBLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
     const size_t rlds = (size_t)(QBA_DBLOCK + qba_def_cols<NP>(0)) * sizeof(uint32_t);
     if (dlds < rlds) dlds = rlds;
     dlds = (dlds + 15) & ~(size_t)15;
@@ -2201,7 +2039,7 @@ int qba_launch_batched(qba_ctx *ctx, const QbaBatch &B) {
   const int samp = sampler_of<NP>(hs);
   if (int rc = check_closed<NP>(hs)) return rc;
   size_t lds = table_lds<NP>(hs, samp) + (size_t)((C::NBP + 3) & ~3) * sizeof(uint32_t);
-  if (QBA_QUEUE) lds += (size_t)(QBA_BLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
+  lds += (size_t)(QBA_BLOCK / 64) * CF<NP>::ND * QBA_QCAP * sizeof(uint32_t) + QBA_QCAP * 4;
   lds = (lds + 15) & ~(size_t)15;
   const int64_t cap = (int64_t)ctx->num_cus * 16;
   // 8-B row vectors (two quads per thread-step; 4 B for nibble rows) when

@@ -4,7 +4,7 @@
 #     tests   pytest -m gpu (whole GPU suite)       smoke   __graft_entry__.smoke()
 #     bench   the driver's command (N=1, --steps 20 --warmup 5), twice
 #     long    bench.py defaults (50 + 200 launches)  c0 c1 c3 c4   bench.py --config k
-#     prof    rocprofv3 --kernel-trace --stats of the driver's command
+#     prof    rocprofv3 --kernel-trace --stats of the driver's command (+ tools/trace_check.py)
 #     profc1  the same for --config 1
 #     pmc     tools/pmc.sh passes of the headline + tools/pmc_traffic.py -> pmc/traffic.json
 #     ab      tools/exp/ab.sh over the experiment builds in _build/exp (ROUNDS=2)
@@ -32,11 +32,14 @@ for s in $steps; do
     c0|c1|c3|c4) timeout -k 10 400 python -u bench.py --config ${s#c} > "$out/bench_config${s#c}.json" \
                    2> "$out/bench_config${s#c}.err" ;;
     prof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o bench \
-             -- python "$root/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > "$out/prof.log" 2>&1) ;;
+             -- python "$root/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > "$out/prof_bench.json" \
+             2> "$out/prof.log")
+          python tools/trace_check.py "$out/prof" "$out/prof_bench.json" > "$out/trace_check.txt" ;;
     profc1) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_c1" \
                -o bench -- python "$root/bench.py" --config 1 --steps 200 --no-cpu-baseline > "$out/prof_c1.log" 2>&1) ;;
     pmc) timeout -k 10 600 bash tools/pmc.sh "gpurun_out/$tag/pmc"
-         python tools/pmc_traffic.py "$out/pmc" 125000000 11 > "$out/pmc/traffic.json" ;;
+         python tools/pmc_traffic.py "$out/pmc" 125000000 11 > "$out/pmc/traffic.json"
+         python tools/pmc_summary.py "$out/pmc" > "$out/pmc/summary.txt" ;;
     ab) ROUNDS=${ROUNDS:-2} timeout -k 10 900 bash tools/exp/ab.sh "$tag/ab" ;;
     cli) timeout -k 10 300 python -u -m tfg---quantum-byzantine-agreement_amd.tfg 1e9 3 --parties 11 --mode count \
            --seed 11 --timing > "$out/cli_count_1e9.txt" 2>&1 ;;
