@@ -260,40 +260,6 @@ struct QbaClosed {
   uint32_t rank, w0;
 };
 
-// Philox4x32-10 on the scalar unit: the same function as qba_philox for
-// wave-uniform arguments, in plain XORs (v_bitop3 has no scalar form)
-__device__ __forceinline__ QbaU4 qba_philox_s(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
-                                              uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-    c1 = (uint32_t)p1;
-    c3 = (uint32_t)p0;
-    c0 = n0;
-    c2 = n2;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return QbaU4{c0, c1, c2, c3};
-}
-
-// The rank of an entry whose two Lemire tests failed: the first accepted word
-// of philox(ctr = {p_lo, p_hi, 0x80000000 + t, h}), t = 1, 2, ... (arguments
-// wave-uniform: scalar unit)
-template <int NP>
-__device__ __forceinline__ uint32_t qba_rank_retry_s(uint32_t plo, uint32_t phi, uint32_t h, uint32_t k0, uint32_t k1) {
-  for (uint32_t t = 1;; ++t) {
-    const QbaU4 y = qba_philox_s(plo, phi, 0x80000000u + t, h, k0, k1);
-    if (qba_accept<NP>(y.x, CF<NP>::T32)) return y.x;
-    if (qba_accept<NP>(y.y, CF<NP>::T32)) return y.y;
-    if (qba_accept<NP>(y.z, CF<NP>::T32)) return y.z;
-    if (qba_accept<NP>(y.w, CF<NP>::T32)) return y.w;
-  }
-}
-
 template <int NP>
 __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64_t p, uint32_t h,
                                                 uint32_t k0, uint32_t k1, QbaClosed &c) {
@@ -311,24 +277,26 @@ __device__ __forceinline__ void qba_closed_rank(uint32_t w0, uint32_t w1, uint64
   // 2^32, 0.56 % at n = 11): the fallback words are chosen inside the rare
   // branch, not by a select on every entry
   uint32_t rank = w1;
-  bool retry = false;
   if (__builtin_expect(!qba_accept<NP>(w1, F::T32), 0)) {
     rank = w0 & ~31u;
-    // both tests failed (P = 6e-4 per entry at n = 11); a not-Q entry's rank
-    // is discarded, so only Q-correlated entries retry
-    retry = !qba_accept<NP>(rank, F::T27) && (w0 & 1u);
-  }
-  // The retries of the wave, lane by lane on the SCALAR unit: no VGPR is
-  // needed, so nothing is spilled.  (Inline, the retry loop pushed the
-  // kernel past its 64 VGPRs: a scratch reload in the loop made the compiler
-  // wait for every outstanding row store -- s_waitcnt vmcnt(0) -- before the
-  // first Philox round of every step.)
-  for (uint64_t m = __ballot(retry); m; m &= m - 1) {  // wave-uniform
-    const int l = __builtin_ctzll(m);
-    const uint32_t r = qba_rank_retry_s<NP>(__builtin_amdgcn_readlane((uint32_t)p, l),
-                                            __builtin_amdgcn_readlane((uint32_t)(p >> 32), l),
-                                            __builtin_amdgcn_readlane(h, l), k0, k1);
-    if ((int)__lane_id() == l) rank = r;
+    // both tests failed (P = 6e-4 per entry at n = 11): words of further
+    // Philox blocks, in order.  A not-Q entry's rank is discarded, so only
+    // Q-correlated entries retry.  (Done lane by lane on the scalar unit
+    // instead, the retry freed the loop of a scratch reload but cost SGPRs
+    // and 2 % more cycles: profiles/r5/ab_retry.)
+    if (!qba_accept<NP>(rank, F::T27) && (w0 & 1u)) {
+      bool ok = false;
+      for (uint32_t t = 1; !ok; ++t) {
+        const QbaU4 y = qba_philox((uint32_t)p, (uint32_t)(p >> 32), 0x80000000u + t, h, k0, k1);
+        const uint32_t cand[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (!ok && qba_accept<NP>(cand[i], F::T32)) {
+            ok = true;
+            rank = cand[i];
+          }
+      }
+    }
   }
   // a not-Q entry discards its table words (qba_closed_finish selects its
   // nibbles): rank 0 sends its three reads to one address per table, served
@@ -873,22 +841,58 @@ __device__ __forceinline__ uint2 qba_pb_pack(const uint32_t (&D)[CF<NP>::ND]) {
   return make_uint2(D[0] | (D[1] << 4), D[2]);
 }
 
-// LDS byte address of pair-bin ring slot s (ring aligned to QBA_QCAP * 8 B)
-__device__ __forceinline__ uint32_t qba_qpb_addr(const QbaWaveQ &q, uint32_t s) {
-  return ((s & (QBA_QCAP - 1)) << 3) | q.base;
-}
-
+// The pair-bin queue is LINEAR: slots [0, qn) of the wave's 128-slot area
+// hold the queued entries.  A push writes slot qn + (queued lanes below this
+// one): ONE v_add_lshl_u32 (the wave's base / 8 rides in the SGPR sum); a
+// drain counts slots [0, nv), one per lane at a loop-invariant address, then
+// moves the leftover (< 64 entries) down to slot 0 with one read (offset
+// 512) and one write per leftover lane.
 template <int NP>
 __device__ __forceinline__ void qba_q_drain_pb(QbaWaveQ &q, uint32_t nv) {
   const uint32_t lane = __lane_id();
   typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-  const v2u c = *reinterpret_cast<__attribute__((address_space(3))) v2u *>(
-      static_cast<uintptr_t>(qba_qpb_addr(q, q.tail + lane)));
+  typedef __attribute__((address_space(3))) v2u lds_v2u;
+  uint32_t a;  // base + 8 lane in one op
+  asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(a) : "v"(lane), "s"(q.base));
+  const v2u c = *reinterpret_cast<lds_v2u *>(static_cast<uintptr_t>(a));
   __builtin_amdgcn_s_setprio(2);  // as qba_q_drain
   if (nv >= 64 || lane < nv) qba_count_pb<NP>(c.x, c.y, q.hoff);
   __builtin_amdgcn_s_setprio(0);
-  q.tail += nv;
   q.qn -= nv;
+  if (q.qn) {  // wave-uniform: the leftover of a full drain (nv = 64)
+    if (lane < q.qn) {
+      const v2u m = *reinterpret_cast<lds_v2u *>(static_cast<uintptr_t>(a + 512u));
+      *reinterpret_cast<lds_v2u *>(static_cast<uintptr_t>(a)) = m;
+    }
+  }
+}
+
+// The lanes whose entry is Q-correlated (L0 != L1, tfg.py:327: byte 0 vs byte
+// 1 of word 0 of the byte layout) among the active lanes `act`: one SDWA
+// v_cmp, then an s_and -- the last writer of the mask is the scalar unit.
+__device__ __forceinline__ uint64_t qba_isq_mask(uint32_t w0, uint64_t act) {
+  uint64_t m;
+  asm("v_cmp_ne_u32_sdwa %0, %1, %1 src0_sel:BYTE_0 src1_sel:BYTE_1\n\ts_and_b64 %0, %0, %2"
+      : "=&s"(m) : "v"(w0), "s"(act));
+  return m;
+}
+
+// Push the entries of the lanes in m (a lane mask, qba_isq_mask)
+template <int NP>
+__device__ __forceinline__ void qba_q_push_pb_m(QbaWaveQ &q, const uint32_t (&D)[CF<NP>::ND], uint64_t m) {
+  const uint32_t mb = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (__builtin_amdgcn_inverse_ballot_w64(m)) {
+    uint32_t a;  // (mb + qn + base / 8) * 8 in one op
+    asm("v_add_lshl_u32 %0, %1, %2, 3" : "=v"(a) : "v"(mb), "s"(q.qn + (q.base >> 3)));
+    const uint2 c = qba_pb_pack<NP>(D);
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    v2u cv;
+    cv.x = c.x;
+    cv.y = c.y;
+    *reinterpret_cast<__attribute__((address_space(3))) v2u *>(static_cast<uintptr_t>(a)) = cv;
+  }
+  q.qn += (uint32_t)__popcll(m);
+  if (q.qn >= 64) qba_q_drain_pb<NP>(q, 64u);
 }
 
 template <int NP>
@@ -896,7 +900,8 @@ __device__ __forceinline__ void qba_q_push_pb(QbaWaveQ &q, const uint32_t (&D)[C
   const uint64_t m = __ballot(isq);
   const uint32_t mb = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
   if (isq) {
-    const uint32_t a = (((mb + q.tail + q.qn) << 3) & (uint32_t)(QBA_QCAP * 8 - 1)) | q.base;
+    uint32_t a;  // (mb + qn + base / 8) * 8 in one op (the compiler splits it into three)
+    asm("v_add_lshl_u32 %0, %1, %2, 3" : "=v"(a) : "v"(mb), "s"(q.qn + (q.base >> 3)));
     const uint2 c = qba_pb_pack<NP>(D);
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     v2u cv;
@@ -1109,6 +1114,7 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
   } else {
     uint32_t Dp[2 * QPT][ND];  // pair p: entries 2p, 2p+1 of the step
     const uint32_t am = act ? 0xffu : 0u;
+    const uint64_t actm = __ballot(act);  // the step's active lanes
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
       qba_sample_quad<NP, SAMP, TAIL, PW>(c0 + 4 * k, valid, first, k0, k1, ps, pat, apat, thr, pl, D);
@@ -1119,14 +1125,22 @@ __device__ __forceinline__ void qba_step_pk(uint32_t c0, uint32_t count, uint64_
       }
       if constexpr (MODE == 1) {
         if constexpr (WQ) {  // the caller's queue (never null)
-          // L0 != L1 (tfg.py:327) of a pair at once: nibble 0 / 1 of
-          // (byte 0 ^ byte 1) of its packed word 0 is entry 2p / 2p+1's test
+          if constexpr (CNT == 1) {
+            // L0 != L1 (tfg.py:327) of each entry: one SDWA compare of byte 0
+            // with byte 1 of its word 0, the step's active lanes ANDed in on
+            // the scalar unit
 #pragma unroll
-          for (int p = 0; p < 2; ++p) {
-            const uint32_t w0 = Dp[2 * k + p][0];
-            const uint32_t x = (w0 ^ (w0 >> 8)) & am;
-            qba_push<NP, true, CNT>(*wq, D[2 * p], (x & 0x0fu) != 0u, hist);
-            qba_push<NP, true, CNT>(*wq, D[2 * p + 1], x > 0x0fu, hist);
+            for (int j = 0; j < 4; ++j) qba_q_push_pb_m<NP>(*wq, D[j], qba_isq_mask(D[j][0], actm));
+          } else {
+            // ... of a pair at once: nibble 0 / 1 of (byte 0 ^ byte 1) of its
+            // packed word 0 is entry 2p / 2p+1's test
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+              const uint32_t w0 = Dp[2 * k + p][0];
+              const uint32_t x = (w0 ^ (w0 >> 8)) & am;
+              qba_push<NP, true, CNT>(*wq, D[2 * p], (x & 0x0fu) != 0u, hist);
+              qba_push<NP, true, CNT>(*wq, D[2 * p + 1], x > 0x0fu, hist);
+            }
           }
         } else {
 #pragma unroll
@@ -1379,7 +1393,8 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
     QbaWaveQ wq;
     if constexpr (CNT) {  // 8-B slots after the pair bins, each ring aligned to its size
       const uint32_t h = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist + QbaPB::AREA * 4;
-      wq.base = ((h + QBA_QCAP * 8 - 1) & ~(uint32_t)(QBA_QCAP * 8 - 1)) + (threadIdx.x >> 6) * (QBA_QCAP * 8);
+      wq.base = __builtin_amdgcn_readfirstlane(((h + QBA_QCAP * 8 - 1) & ~(uint32_t)(QBA_QCAP * 8 - 1)) +
+                                               (threadIdx.x >> 6) * (QBA_QCAP * 8));
     } else {
       wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
     }
