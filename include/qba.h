@@ -145,8 +145,14 @@ QBA_API int qba_check_counts(qba_ctx *ctx, int n_parties, const uint8_t *lists_d
 /* Statistics of the last counts launch on this ctx (synchronous):
  * out[0] = Q-correlated entries that held a value >= w and were therefore
  * not counted (never happens for lists from qba_sample); out[1] = workgroups
- * of the fused n = 11 kernel whose 8-bit pair bins wrapped and that recounted
- * their entries exactly from the stored rows (0 unless forced: QBA_LIST_GRID). */
+ * of an n = 11 pair-bin kernel (the fused kernel from 2^24 entries, the
+ * check of nibble rows) whose 8-bit pair bins wrapped and that recounted
+ * their entries exactly from the stored rows.  Pair-bin launches give a
+ * workgroup at most 2^18 entries (a larger call is split, later parts
+ * accumulating), where no bin wraps for sampled lists; the environment
+ * variables the tests use to force wraps and pair bins on small launches
+ * (QBA_LIST_GRID = workgroups per launch, QBA_PB_MIN_ENTRIES) keep a
+ * workgroup below 2^23 entries, so a wrap is always detected exactly. */
 QBA_API int qba_last_stats(qba_ctx *ctx, int64_t *out2_host);
 /* Fused sample + check: lists are written once and counted from registers. */
 QBA_API int qba_sample_check(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
@@ -156,7 +162,9 @@ QBA_API int qba_sample_check(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_
 /* The same three passes over packed (nibble-row) lists; counts identical to
  * the byte-layout calls on the same entries.  qba_check_counts_packed cannot
  * see a value > 15 (not representable); values in [w, 15] are caught as in
- * qba_check_counts (qba_last_stats). */
+ * qba_check_counts (qba_last_stats).  Every counting call tests Cond3
+ * (tfg.py:96-98) on every Q-correlated entry: an entry whose values are not
+ * pairwise distinct adds its equal pairs to C[u][g][h]. */
 QBA_API int qba_sample_packed(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first, uint64_t count,
                               uint8_t *packed_dev, uint64_t ld, qba_stream stream);
 QBA_API int qba_sample_check_packed(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
@@ -171,13 +179,14 @@ QBA_API int qba_check_counts_packed(qba_ctx *ctx, int n_parties, const uint8_t *
  * 68-84, 182, 189, 291-294, 327, consistent() 87-98), but the call's H, C, P
  * and qba_last_stats are complete only after the NEXT deferred call on this
  * ctx or qba_flush_deferred(ctx): the next call's list kernel reduces this
- * call's slab rows in workgroups of its own (two alternating slab buffers):
- * ahead of its list workgroups for small calls, after them -- in the slots
- * its early-finishing workgroups free -- for the pair-bin kernel of large n =
- * 11 calls.  A small call whose list workgroups fill the chip, any
- * non-deferred counting call and qba_reserve flush the pending reduction
- * first; a pending call on another stream is flushed there and ordered by an
- * event. */
+ * call's slab rows in workgroups of its own (two alternating slab buffers),
+ * dispatched after its list workgroups into the CUs they leave idle.  A
+ * small call whose list workgroups fill the chip, any non-deferred counting
+ * call and qba_reserve flush the pending reduction first; a pending call on
+ * another stream is flushed there and ordered by an event.  A pair-bin call
+ * larger than one launch's per-workgroup budget (above ~1.3e8 entries at n =
+ * 11) runs its earlier parts synchronously and defers only its last part's
+ * reduction. */
 QBA_API int qba_sample_check_deferred(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
                                       uint64_t count, uint8_t *lists_dev, uint64_t ld, int64_t *H_dev,
                                       int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);
