@@ -1368,7 +1368,7 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   using C = QCfg<NP>;
   extern __shared__ __align__(16) uint64_t lds[];
   // list workgroups: [red, gridDim.x - tail) (reduce workgroups of a
-  // deferred reduction ahead of them, qba_k_lists_def, or after them,
+  // deferred reduction after them, qba_k_lists_def and
   // qba_k_lists_pbdef)
   const uint32_t bid = blockIdx.x - red, nblk = gridDim.x - red - tail;
   const uint64_t *pat, *apat, *thr;
@@ -1388,7 +1388,11 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   // scalar load whose s_waitcnt lgkmcnt(0) also drains every LDS atomic the
   // wave has in flight (-2% step time)
   const uint32_t ustride = __builtin_amdgcn_readfirstlane(nblk * BS);
-  const uint32_t u0 = bid * BS + threadIdx.x;
+  // unit u of a step: wave-major over the grid (wave w of workgroup b takes
+  // units [(w nblk + b) 64, +64)), so a launch with fewer units than threads
+  // spreads them over every workgroup instead of filling the first ones;
+  // a wave's 64 units stay consecutive (one 256-B / 512-B store per row)
+  const uint32_t u0 = ((threadIdx.x >> 6) * nblk + bid) * 64u + (threadIdx.x & 63u);
   if constexpr (MODE != 0) {
     QbaWaveQ wq;
     if constexpr (CNT) {  // 8-B slots after the pair bins, each ring aligned to its size
@@ -1499,7 +1503,7 @@ __global__ void QBA_LISTS_BOUNDS
 struct QbaDefer {
   const uint32_t *slab;  // the pending call's slab rows (NBP words apart)
   int rows;              // its list workgroups
-  int red;               // reduce workgroups ahead of the list workgroups: W, or 0 (none pending)
+  int red;               // reduce workgroups after the list workgroups: W, or 0 (none pending)
   int acc;               // the pending call accumulates into its outputs
   int sacc;              // ... and into the stats (a later chunk of one call)
   int64_t *H, *C, *P, *stats;
@@ -1600,7 +1604,10 @@ __device__ __forceinline__ void qba_reduce_u(const QbaDefer &d, int u, int part,
 }
 
 // Sample + check (MODE 1) with the pending deferred call's reduction in the
-// first d.red workgroups; the list workgroups follow (slab row = their index).
+// LAST d.red workgroups: the list workgroups (slab row = their index) are
+// dispatched first, the reduce workgroups into the CUs they leave idle
+// (configs[1]: 9.42-9.47 vs 9.68-10.27 us per pass with the reduction ahead,
+// profiles/r5/c1)
 template <int NP, int SAMP, int QPT, int PK>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, QBA_DBLOCK),
                                amdgpu_waves_per_eu(SAMP == QBA_S_CLOSED ? QBA_DEF_WAVES : 1)))
@@ -1608,14 +1615,15 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, QBA_DBLOCK),
                     uint32_t count, uint8_t *__restrict__ lists, uint64_t ld, uint32_t *__restrict__ slab,
                     QbaZero zero, QbaDefer d) {
   extern __shared__ __align__(16) uint64_t lds[];
-  if ((int)blockIdx.x < d.red) {  // workgroup-uniform
+  const uint32_t nl = gridDim.x - (uint32_t)d.red;
+  if (blockIdx.x >= nl) {  // workgroup-uniform
     constexpr int NP4 = qba_def_parts<NP>();
-    qba_reduce_u<NP>(d, (int)blockIdx.x / NP4, (int)blockIdx.x % NP4, (int)threadIdx.x, QBA_DBLOCK,
-                     reinterpret_cast<uint32_t *>(lds));
+    const int r = (int)(blockIdx.x - nl);
+    qba_reduce_u<NP>(d, r / NP4, r % NP4, (int)threadIdx.x, QBA_DBLOCK, reinterpret_cast<uint32_t *>(lds));
     return;
   }
   qba_lists_body<NP, 1, SAMP, QPT, PK, QBA_DBLOCK, 0, QBA_DEF_PAIRWISE>(ps, k0, k1, first, count, lists,
-                                                                                   ld, slab, zero, (uint32_t)d.red);
+                                                                                   ld, slab, zero, 0u, (uint32_t)d.red);
 }
 
 // qba_flush_deferred: the last pending reduction on its own.
@@ -1938,7 +1946,7 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   uint8_t *lists = L.lists;
   uint64_t ld = L.ld;
   // Deferred reduction: the list kernel also reduces the pending deferred
-  // call (W workgroups ahead of its own) when both fit the chip's resident
+  // call (W workgroups after its own) when both fit the chip's resident
   // slots together; otherwise the pending one is flushed and this call is
   // reduced at once (its results are then simply complete earlier).
   const void *kd = nullptr;
@@ -1979,6 +1987,10 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
     dlds = (dlds + 15) & ~(size_t)15;
     if (dlds > 65536) QBA_HIP(hipFuncSetAttribute(kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds));
     dgrid = grid_for(ctx, kd, dlds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1, &dcap, QBA_DBLOCK);
+    // a launch that would leave CUs idle spreads its units over one workgroup
+    // per CU (wave-major units, qba_lists_body): the LDS work of its counting
+    // is what bounds it (configs[1]: 163 -> 256 workgroups)
+    if (dgrid < ctx->num_cus && ctx->num_cus + qba_def_wgs<NP>() <= dcap) dgrid = ctx->num_cus;
   }
   if (kd && (pbd || dgrid + qba_def_wgs<NP>() <= dcap)) {
     const int grid = dgrid;
