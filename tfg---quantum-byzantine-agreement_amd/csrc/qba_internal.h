@@ -107,9 +107,10 @@ struct QbaProgram {
   QbaFactor fac[QBA_MAX_FACTORS];
 };
 
-// Device image of the compiled programs for one n: [prog notq][prog q]
-// followed by pat[T], apat[T], thr[T] (uint64) where T = total table entries
-// (notq tables first).
+// Device image of the compiled programs for one n: [prog notq][prog q], the
+// closed-form stage tables (16-B words, at QBA_PERM_OFF), then pat[T],
+// apat[T], thr[T] (uint64, at tab_off) where T = total table entries (notq
+// tables first).
 struct QbaProgramSet {
   QbaProgram prog[2];
   int32_t table_total;
@@ -130,9 +131,14 @@ struct QbaProgramSet {
   uint32_t t32;             // 2^32 mod n!  (Lemire rejection threshold, 32-bit)
   uint32_t nfact;           // n!
   uint32_t ra, rb, rc;      // stage sizes, ra * rb * rc = n!
-  int32_t perm_off;         // byte offset of the stage tables from the image start
+  int32_t perm_off;         // byte offset of the stage tables from the image start (QBA_PERM_OFF)
   int32_t perm_words;       // u32 words of stage tables: A [ra][4], B [rb][2], C [rc] (hi only)
+  int32_t tab_off;          // byte offset of pat / apat / thr (after the stage tables)
 };
+// The stage tables sit right after the header, at an offset the list kernels
+// know at compile time: their first table loads need no scalar load of the
+// header first (one memory round trip less at each workgroup's start).
+#define QBA_PERM_OFF ((sizeof(QbaProgramSet) + 15) & ~(size_t)15)
 
 // Closed-form stage tables (host-built, staged to LDS): 4 + 2 + 1 words per
 // entry of A, B, C.  Largest: n = 11 -> 990*4 + 1680*2 + 24 = 7344 words.

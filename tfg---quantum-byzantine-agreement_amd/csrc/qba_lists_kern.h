@@ -1221,7 +1221,8 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
   pl = reinterpret_cast<const uint32_t *>(lds);
   uint32_t *hist = reinterpret_cast<uint32_t *>(lds);
   if constexpr (MODE != 2 && SAMP == QBA_S_CLOSED) {
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + ps->perm_off);
+    // at a compile-time offset: the loads issue without reading the header
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + QBA_PERM_OFF);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
     // 16-B loads, all issued before the first LDS write: one memory round
     // trip per workgroup instead of one per word-loop iteration (the image
@@ -1239,7 +1240,7 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
     hist = dst + ((CF<NP>::WORDS + 3) & ~3);
   } else if constexpr (MODE != 2) {
     const int T = ps->table_total;
-    const uint64_t *tab = reinterpret_cast<const uint64_t *>(ps + 1);
+    const uint64_t *tab = reinterpret_cast<const uint64_t *>(reinterpret_cast<const char *>(ps) + ps->tab_off);
     const int ntab = ps->any_nonuniform ? 3 * T : T;
     for (int i = threadIdx.x; i < ntab; i += BS) lds[i] = tab[i];
     apat = lds + T;
@@ -1845,7 +1846,8 @@ static size_t table_lds(const QbaProgramSet *hs, int samp) {
 template <int NP>
 static int check_closed(const QbaProgramSet *hs) {
   if (hs->closed && (hs->ra != CF<NP>::RA || hs->rb != CF<NP>::RB || hs->rc != CF<NP>::RC ||
-                     hs->perm_words != CF<NP>::WORDS || hs->t32 != CF<NP>::T32))
+                     hs->perm_words != CF<NP>::WORDS || hs->t32 != CF<NP>::T32 ||
+                     hs->perm_off != (int32_t)QBA_PERM_OFF))
     return qba_fail(QBA_EINVAL, "closed-form program does not match the kernel's stage layout");
   return QBA_OK;
 }

@@ -375,8 +375,9 @@ int qba_plan_image(int n, const QbaHostProgram &a, const QbaHostProgram &b, std:
   if (pw.size() > QBA_PERM_MAX_WORDS) return qba_fail(QBA_EINVAL, "permutation tables too large");
   // stage tables 16-B aligned and padded to whole 16-B words: the list kernels
   // stage them into LDS with 16-B loads
-  const size_t perm_off = (sizeof(QbaProgramSet) + 3 * sizeof(uint64_t) * (size_t)T + 15) & ~(size_t)15;
-  img.assign(perm_off + sizeof(uint32_t) * ((pw.size() + 3) & ~(size_t)3), 0);
+  const size_t perm_off = QBA_PERM_OFF;
+  const size_t tab_off = perm_off + sizeof(uint32_t) * ((pw.size() + 3) & ~(size_t)3);
+  img.assign(tab_off + 3 * sizeof(uint64_t) * (size_t)T, 0);
   QbaProgramSet *ps = reinterpret_cast<QbaProgramSet *>(img.data());
   ps->prog[0] = a.p;
   ps->prog[1] = b.p;
@@ -402,17 +403,18 @@ int qba_plan_image(int n, const QbaHostProgram &a, const QbaHostProgram &b, std:
       ps->canonical = 0;
   }
   ps->closed = closed ? 1 : 0;
+  ps->perm_off = (int32_t)perm_off;
+  ps->tab_off = (int32_t)tab_off;
   if (closed) {
     ps->nfact = (uint32_t)factorial(n);
     ps->t32 = (uint32_t)((1ull << 32) % ps->nfact);
     ps->ra = ra;
     ps->rb = rb;
     ps->rc = rc;
-    ps->perm_off = (int32_t)perm_off;
     ps->perm_words = (int32_t)pw.size();
     if (!pw.empty()) memcpy(img.data() + perm_off, pw.data(), sizeof(uint32_t) * pw.size());
   }
-  uint64_t *tab = reinterpret_cast<uint64_t *>(ps + 1);
+  uint64_t *tab = reinterpret_cast<uint64_t *>(img.data() + tab_off);
   std::copy(a.pat.begin(), a.pat.end(), tab);
   std::copy(b.pat.begin(), b.pat.end(), tab + a.pat.size());
   std::copy(a.apat.begin(), a.apat.end(), tab + T);

@@ -123,6 +123,10 @@ static void check_circuits(std::mt19937_64 &rng) {
     if (ps->closed)  // the list kernels stage the tables with 16-B loads of whole 16-B words
       CHECK(ps->perm_off % 16 == 0 && img.size() >= (size_t)ps->perm_off + 16 * (((size_t)ps->perm_words + 3) / 4),
             "stage tables not 16-B aligned / padded n=%d", n);
+    CHECK(ps->perm_off == (int32_t)QBA_PERM_OFF && ps->tab_off % 16 == 0 &&
+              ps->tab_off >= ps->perm_off + 16 * ((ps->perm_words + 3) / 4) &&
+              img.size() == (size_t)ps->tab_off + 24 * (size_t)ps->table_total,
+          "image layout n=%d", n);
     // malformed circuits
     std::vector<int32_t> bad = q_gates(n, perm), kept;
     if (n >= 2) {

@@ -19,7 +19,8 @@ N=${N:-11}
 out=${EXPOUT:-$here/../_build/exp}; mkdir -p $out
 F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -fvisibility=hidden -munsafe-fp-atomics -I$here -I$here/../../include -DQBA_EXPERIMENT_BUILD"
 /opt/rocm/bin/hipcc $F -DQBA_ONLY_N=$N "$@" -c $src/qba_lists.hip -o $out/$name.o
-/opt/rocm/bin/hipcc $F -DQBA_INST_N=$N "$@" -c $src/qba_lists_inst.hip -o $out/${name}_n$N.o
+# the shipped list kernels take their arguments preloaded (csrc/Makefile PRELOAD)
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-kernarg-preload-count=16 -DQBA_INST_N=$N "$@" -c $src/qba_lists_inst.hip -o $out/${name}_n$N.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/$name.so $out/$name.o $out/${name}_n$N.o \
   $here/../_build/qba_ctx.o $here/../_build/qba_exact.o $here/../_build/qba_sv.o $here/../_build/qba_resource.o \
   $here/../_build/qba_rccl.o $here/../_build/qba_plan.o $here/../_build/qba_host.o -ldl
