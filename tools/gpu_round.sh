@@ -7,6 +7,7 @@
 #     prof    rocprofv3 --kernel-trace --stats of the driver's command (+ tools/trace_check.py)
 #     profc1  the same for --config 1
 #     pmc     tools/pmc.sh passes of the headline + tools/pmc_traffic.py -> pmc/traffic.json
+#     pmcset  copy that file to profiles/traffic_n11.json (later bench steps report its traffic)
 #     ab      tools/exp/ab.sh over the experiment builds in _build/exp (ROUNDS=2)
 #     cli     the count-mode CLI at sizeL = 1e9 in a fresh process
 # Default: tests smoke bench prof.  Every GPU step has its own time limit; the
@@ -40,6 +41,7 @@ for s in $steps; do
     pmc) timeout -k 10 600 bash tools/pmc.sh "gpurun_out/$tag/pmc"
          python tools/pmc_traffic.py "$out/pmc" 125000000 11 > "$out/pmc/traffic.json"
          python tools/pmc_summary.py "$out/pmc" > "$out/pmc/summary.txt" ;;
+    pmcset) cp "$out/pmc/traffic.json" profiles/traffic_n11.json ;;  # the box's bench steps then report it
     ab) ROUNDS=${ROUNDS:-2} timeout -k 10 900 bash tools/exp/ab.sh "$tag/ab" ;;
     cli) timeout -k 10 300 python -u -m tfg---quantum-byzantine-agreement_amd.tfg 1e9 3 --parties 11 --mode count \
            --seed 11 --timing > "$out/cli_count_1e9.txt" 2>&1 ;;
