@@ -82,7 +82,6 @@ extern "C" int qba_destroy(qba_ctx *ctx) {
   if (ctx->zc_pending) (void)hipEventSynchronize(ctx->zc_ev);
   if (ctx->zc_ev) (void)hipEventDestroy(ctx->zc_ev);
   if (ctx->def_ev) (void)hipEventDestroy(ctx->def_ev);
-  if (ctx->slab_ev) (void)hipEventDestroy(ctx->slab_ev);
   if (ctx->zc) (void)hipHostFree(ctx->zc);
   if (ctx->pin_h) (void)hipHostFree(ctx->pin_h);
   if (ctx->pin_d) (void)hipFree(ctx->pin_d);

@@ -209,13 +209,12 @@ struct qba_ctx {
   // recorded inside a capture, with that capture's id
   int pend_captured = 0;
   unsigned long long pend_capture_id = 0;
-  // the slab's last user (qba_slab_order / qba_slab_done): an event recorded
-  // on its stream after its launches, and that stream's handle as a VALUE only
-  // (compared, never passed to HIP: the stream may be destroyed since); a
-  // counting launch on another stream waits for the event
-  hipEvent_t slab_ev = nullptr;
+  // the slab's last user (qba_slab_order / qba_slab_done): its stream's
+  // handle as a VALUE only (compared, never passed to HIP: the stream may be
+  // destroyed since); a counting launch on another stream synchronises the
+  // device first
   uintptr_t slab_last = 0;
-  bool slab_ev_set = false;
+  bool slab_set = false;
 };
 // Capture state of a stream: 1 capturing (its capture id in *id), 0 not.
 int qba_capture_of(hipStream_t s, unsigned long long *id);

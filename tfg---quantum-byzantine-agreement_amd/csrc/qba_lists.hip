@@ -171,25 +171,25 @@ static int pend_capture_ok(qba_ctx *ctx, hipStream_t s) {
 
 // Only eager streams are ordered here: inside a capture the graph's own
 // dependencies order its nodes, and across a capture boundary the caller
-// synchronises (include/qba.h) -- an eager event cannot be waited on by a
-// capturing stream, and a captured launch records no event.  The previous
-// user's stream is never touched: the event was recorded on it while it was
-// known to exist (qba_slab_done), so destroying that stream since is safe.
+// synchronises (include/qba.h).  The previous user's stream is never touched
+// (it may be destroyed since): a counting launch on another stream than the
+// previous one synchronises the device, which completes that stream's work.
+// A stream switch is rare; an event recorded after every counting launch
+// instead put a ~6 us marker between each launch and the next on the same
+// stream (profiles/r5/slab_event).
 int qba_slab_order(qba_ctx *ctx, hipStream_t stream) {
   unsigned long long id = 0;
-  if (ctx->slab_ev_set && ctx->slab_last != reinterpret_cast<uintptr_t>(stream) && !qba_capture_of(stream, &id))
-    QBA_HIP(hipStreamWaitEvent(stream, ctx->slab_ev, 0));
+  if (ctx->slab_set && ctx->slab_last != reinterpret_cast<uintptr_t>(stream) && !qba_capture_of(stream, &id)) {
+    QBA_HIP(hipDeviceSynchronize());
+    ctx->slab_set = false;
+  }
   return QBA_OK;
 }
 
 int qba_slab_done(qba_ctx *ctx, hipStream_t stream) {
   unsigned long long id = 0;
-  ctx->slab_ev_set = false;
-  if (qba_capture_of(stream, &id)) return QBA_OK;
-  if (!ctx->slab_ev) QBA_HIP(hipEventCreateWithFlags(&ctx->slab_ev, hipEventDisableTiming));
-  QBA_HIP(hipEventRecord(ctx->slab_ev, stream));
+  ctx->slab_set = !qba_capture_of(stream, &id);
   ctx->slab_last = reinterpret_cast<uintptr_t>(stream);
-  ctx->slab_ev_set = true;
   return QBA_OK;
 }
 

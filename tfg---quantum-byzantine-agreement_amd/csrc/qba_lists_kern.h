@@ -1273,12 +1273,11 @@ __device__ __forceinline__ void qba_zero_outputs(const QbaZero &z, int tid, int 
 // wrapped; the slab row is then left to the caller's recount.  Slab words of
 // group 1 and the row padding are not written (the reductions skip them).
 template <int NP, int BS>
-__device__ __forceinline__ bool qba_pb_flush(uint32_t *hist, uint32_t *row) {
+__device__ __forceinline__ bool qba_pb_flush(uint32_t *hist, uint32_t *row, int t) {
   using C = QCfg<NP>;
   static_assert(BS >= 512, "four roles of 256 threads");
   const uint32_t *A = hist, *Bw = hist + QbaPB::BOFF;
   uint32_t *misc = hist + QbaPB::WORDS;
-  const int t = threadIdx.x;
   uint32_t v[5] = {0u, 0u, 0u, 0u, 0u}, g0 = 0u;
   const int ug = (t & 255) >> 4, xg = t & 15;    // column-sum threads: (u, x)
   const int ur = t & 15, yr = (t & 255) >> 4;    // row-sum threads: (u, y), u fastest
@@ -1394,6 +1393,12 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   // spreads them over every workgroup instead of filling the first ones;
   // a wave's 64 units stay consecutive (one 256-B / 512-B store per row)
   const uint32_t u0 = ((threadIdx.x >> 6) * nblk + bid) * 64u + (threadIdx.x & 63u);
+  // the wave's index in an SGPR: the code after the main loop rebuilds the
+  // thread index from it and the lane id instead of keeping threadIdx.x (and
+  // what derives from it) live across the loop -- at 64 VGPRs those values
+  // were spilled to scratch, and a kernel with scratch waits ~6 us longer for
+  // its dispatch after the previous kernel (profiles/r5/noscratch)
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if constexpr (MODE != 0) {
     QbaWaveQ wq;
     if constexpr (CNT) {  // 8-B slots after the pair bins, each ring aligned to its size
@@ -1425,10 +1430,11 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
       qba_step_l<NP, MODE, SAMP, QPT, false, PK, false, 0, PW>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat,
                                                             thr, pl, lists, ld, hist);
   }
+  const uint32_t tid = (wv << 6) | __lane_id();  // == threadIdx.x (above)
   // the remaining < 4 QPT entries: whole quads, then the partial one
   const uint32_t r0 = nunits * (4 * QPT), rq = (count - r0 + 3) >> 2;
-  if (bid == nblk - 1 && threadIdx.x < rq) {
-    const uint32_t c0 = r0 + 4 * threadIdx.x;
+  if (bid == nblk - 1 && tid < rq) {
+    const uint32_t c0 = r0 + 4 * tid;
     if (c0 + 4 <= count)
       qba_step_l<NP, MODE, SAMP, 1, false, PK, false, CNT, PW>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists, ld, hist);
     else
@@ -1439,20 +1445,20 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
     uint32_t *row = slab + (size_t)bid * C::NBP;
     bool classic = !CNT;
     if constexpr (CNT) {
-      if (qba_pb_flush<NP, BS>(hist, row)) {
+      if (qba_pb_flush<NP, BS>(hist, row, (int)tid)) {
         // a pair-bin lane wrapped (never for sampled lists at QBA_PB_BUDGET
         // entries per workgroup): recount this workgroup's entries -- the
         // same units and tail as above -- from the rows it stored, into the
         // classic 32-bit bins (qba_count_quad: exact, order-free)
         __syncthreads();
-        for (int i = threadIdx.x; i < C::NBP; i += BS) hist[i] = 0u;
+        for (int i = tid; i < C::NBP; i += BS) hist[i] = 0u;
         __threadfence();  // this workgroup's list stores are complete and visible to its loads
         __syncthreads();
-        for (uint32_t u = u0; u < nunits; u += ustride)
+        for (uint32_t u = ((wv * nblk + bid) << 6) | __lane_id(); u < nunits; u += ustride)
           qba_step_l<NP, 2, QBA_S_GENERAL, QPT, false, PK>(u * (4 * QPT), count, first, k0, k1, ps, pat, apat, thr,
                                                          pl, lists, ld, hist);
-        if (bid == nblk - 1 && threadIdx.x < rq) {
-          const uint32_t c0 = r0 + 4 * threadIdx.x;
+        if (bid == nblk - 1 && tid < rq) {
+          const uint32_t c0 = r0 + 4 * tid;
           if (c0 + 4 <= count)
             qba_step_l<NP, 2, QBA_S_GENERAL, 1, false, PK>(c0, count, first, k0, k1, ps, pat, apat, thr, pl, lists,
                                                          ld, hist);
@@ -1461,18 +1467,18 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
                                                         ld, hist);
         }
         __syncthreads();
-        if (threadIdx.x == 0) hist[C::HBL + C::CBL + 1] += 1u;  // stats[1]: recounting workgroups
+        if (tid == 0) hist[C::HBL + C::CBL + 1] += 1u;  // stats[1]: recounting workgroups
         classic = true;
       }
     }
     if (classic) {
       uint4 *dst = reinterpret_cast<uint4 *>(row);
       const uint4 *src = reinterpret_cast<const uint4 *>(hist);
-      for (int i = threadIdx.x; i < C::NBP / 4; i += BS) dst[i] = src[i];
+      for (int i = tid; i < C::NBP / 4; i += BS) dst[i] = src[i];
     }
     // any point of this kernel precedes the reduction; at the end it leaves
     // the main loop's code placement alone
-    if (bid == nblk - 1) qba_zero_outputs<NP>(zero, threadIdx.x, BS);
+    if (bid == nblk - 1) qba_zero_outputs<NP>(zero, tid, BS);
   }
 }
 

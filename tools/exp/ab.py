@@ -30,5 +30,11 @@ L.sort()
 us = [(e - s) / 1e3 for s, e in L]
 win = st.mean(us[5:25]) if len(us) >= 25 else float("nan")
 steady = st.mean(us[200:300]) if len(us) >= 300 else float("nan")
+# step = start to start of consecutive list kernels: the kernel, the reduce
+# launch and the dispatch gaps between them
+step = [(L[i + 1][0] - L[i][0]) / 1e3 for i in range(len(L) - 1)]
+swin = st.mean(step[5:24]) if len(step) >= 25 else float("nan")
+ssteady = st.mean(step[200:299]) if len(step) >= 299 else float("nan")
 print(f"{name:24s} cycles/launch {cyc:9.0f}  VALU/entry {valu:6.1f}  LDS-instr/entry {lds:5.2f}  "
-      f"LDS busy {ldsbusy:4.2f} conflicts {conf:4.2f}  |  us: window {win:6.1f}  steady {steady:6.1f}")
+      f"LDS busy {ldsbusy:4.2f} conflicts {conf:4.2f}  |  us: window {win:6.1f}  steady {steady:6.1f}"
+      f"  | step: window {swin:6.1f}  steady {ssteady:6.1f}")

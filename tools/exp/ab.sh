@@ -18,5 +18,11 @@ for r in $(seq 1 ${ROUNDS:-1}); do
     QBA_LIB=$so timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $out/$name.$r.tr -o t -- \
         python $root/bench.py --no-cpu-baseline --steps 300 --warmup 0 "$@" > $out/$name.$r.tr.log 2>&1
     python $root/tools/exp/ab.py $out/$name.$r $name | tee -a $out/summary.txt
+    # the driver's command (window only, events around the 20 timed launches)
+    QBA_LIB=$so timeout -k 10 120 python $root/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline "$@" \
+        > $out/$name.$r.drv.json 2> $out/$name.$r.drv.err
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); \
+print(f'{sys.argv[2]:24s} driver command {d[\"ms_per_step\"]*1e3:6.1f} us/step')" $out/$name.$r.drv.json $name \
+        | tee -a $out/summary.txt
   done
 done
