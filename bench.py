@@ -247,17 +247,20 @@ def headline(args):
     packed = args.layout == "packed"
     lists = eng.alloc_packed(n, per) if packed else eng.alloc_lists(n, per)
     _, _, _, total = dist_mod.count_layout(n)
-    # QBA_BENCH_DEFER=1: the fused packed step defers its count reduction
-    # into the NEXT step's list kernel (qba_sample_check_packed_deferred: the
-    # pair-bin kernel runs the pending reduction in workgroups after its own),
-    # so step i's counts are complete once step i+1 is enqueued, and the last
-    # step's after the flush -- all inside the timed region.  Measured equal
-    # to the synchronous step (0.343-0.360 vs 0.353 ms/step, interleaved on
-    # one box, profiles/r4/tail_defer/), so the default stays synchronous.
+    # The fused packed step defers its count reduction into the NEXT step's
+    # list kernel (qba_sample_check_packed_deferred: the pair-bin kernel runs
+    # the pending reduction in workgroups after its own, dispatched into the
+    # CUs its last list workgroups leave idle), so step i's counts are
+    # complete once step i+1 is enqueued, and the last step's after the
+    # flush -- all inside the timed region, and checked against the golden
+    # totals below.  One kernel per step instead of list kernel + reduce
+    # launch: steady step 277.9 -> 271.9 us, the driver's window 352.5 ->
+    # 344.4 us in rocprofv3 traces of one box (profiles/r5/defer/).
+    # QBA_BENCH_DEFER=0 restores the synchronous step.
     # N > 1: a step's all-reduce runs asynchronously (RCCL's own stream) as
     # soon as its counts are complete; a count buffer is written again only
     # after its all-reduce was waited for.
-    deferred = packed and args.mode == "fused" and os.environ.get("QBA_BENCH_DEFER", "0") == "1"
+    deferred = packed and args.mode == "fused" and os.environ.get("QBA_BENCH_DEFER", "1") == "1"
     nbuf = 3 if world > 1 else 1
     flats = [torch.zeros(total, dtype=torch.int64, device=eng.device) for _ in range(nbuf)]
     counts = [eng_mod.Counts(*dist_mod.split_counts(f, n)) for f in flats]

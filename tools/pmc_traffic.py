@@ -26,7 +26,9 @@ layout = sys.argv[5] if len(sys.argv) > 5 else "packed"
 vals = {}
 for f in root.glob("p*/**/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith(f"void qba_k_lists<{n}, 1"):
+        # the synchronous step's list kernel, or the deferred step's (bench.py's
+        # default: the previous step's reduction in its tail)
+        if r["Kernel_Name"].startswith((f"void qba_k_lists<{n}, 1", f"void qba_k_lists_pbdef<{n},")):
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 fetch = statistics.median(vals["FETCH_SIZE"]) * 1024 * 2
 # the issue side of the same kernel (the other tools/pmc.sh passes): per-launch
@@ -43,7 +45,7 @@ out = {"n": n, "per_launch_entries": per, "mode": mode, "layout": layout,
        "write_calibration": {"known_list_bytes": known, "write_over_known": write / known},
        "algorithmic_bytes_per_launch": known,  # the lists written once (bench.py roofline.achieved)
        "metric_scale_bytes_per_launch": 2 * (n + 1) * per,  # BASELINE's 2(n+1) B per entry convention
-       "source": str(root), "kernel": f"qba_k_lists<{n},1,*>",
+       "source": str(root), "kernel": f"qba_k_lists<{n},1,*> / qba_k_lists_pbdef<{n},*>",
        "issue_counters_per_launch": issue,
        # the library the counters were read from: bench.py drops the figure for any other build
        "libqba_sha16": hashlib.sha256(open(os.environ.get("QBA_LIB", Path(__file__).resolve().parent.parent
