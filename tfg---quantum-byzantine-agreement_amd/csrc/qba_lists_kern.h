@@ -1224,19 +1224,26 @@ __device__ __forceinline__ uint32_t *qba_stage(const QbaProgramSet *__restrict__
     // at a compile-time offset: the loads issue without reading the header
     const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(ps) + QBA_PERM_OFF);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
-    // 16-B loads, all issued before the first LDS write: one memory round
-    // trip per workgroup instead of one per word-loop iteration (the image
-    // pads the tables to whole 16-B words, qba_plan_image)
+    // 16-B buffer loads, all issued before the first LDS write: one memory
+    // round trip per workgroup (the image pads the tables to whole 16-B
+    // words, qba_plan_image).  A buffer load past the tables' W4 words returns
+    // zero, so every lane loads unconditionally at a 32-bit offset; only the
+    // LDS writes are guarded.  (Plain loads with a guard were serialised by
+    // the compiler -- load, wait, write, per word -- or went to scratch.)
     constexpr int W4 = (CF<NP>::WORDS + 3) / 4, PER = (W4 + BS - 1) / BS;
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(src), (short)0, W4 * 16, 0x00020000);
+    v4u v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (threadIdx.x + k * BS) * 16u, 0, 0);
+    // the guarded writes' loads are not sunk into their branches
+#pragma unroll
+    for (int k = 0; k < PER; ++k) asm volatile("" ::"v"(v[k]));
     uint4 *d4 = reinterpret_cast<uint4 *>(dst);
-    uint4 v[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (threadIdx.x + k * BS < W4) v[k] = s4[threadIdx.x + k * BS];
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-      if (threadIdx.x + k * BS < W4) d4[threadIdx.x + k * BS] = v[k];
+      if (threadIdx.x + k * BS < W4) d4[threadIdx.x + k * BS] = make_uint4(v[k].x, v[k].y, v[k].z, v[k].w);
     hist = dst + ((CF<NP>::WORDS + 3) & ~3);
   } else if constexpr (MODE != 2) {
     const int T = ps->table_total;
@@ -1678,8 +1685,9 @@ __global__ void __launch_bounds__(QBA_BLOCK)
   const uint64_t *pat, *apat, *thr;
   const uint32_t *pl;
   uint32_t *hist = qba_stage<NP, 1, SAMP, QBA_BLOCK>(ps, lds, pat, apat, thr, pl);
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int64_t inst = blockIdx.x; inst < n_inst; inst += gridDim.x) {
-    for (int i = threadIdx.x; i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
+    for (int i = (int)((wv << 6) | __lane_id()); i < C::NBINS; i += QBA_BLOCK) hist[i] = 0u;
     __syncthreads();
     const uint64_t key = seed_base + (uint64_t)inst;
     const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
@@ -1688,21 +1696,24 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     // per-wave LDS queue (as qba_k_lists), then the < 4 QPT remaining entries
     const uint32_t nunits = (uint32_t)count / (4 * QPT);
     QbaWaveQ wq;
-    wq.base = qba_queue_base<NP>(hist) + (threadIdx.x >> 6) * (CF<NP>::ND * QBA_QCAP * 4);
+    wq.base = qba_queue_base<NP>(hist) + wv * (CF<NP>::ND * QBA_QCAP * 4);
     wq.tail = 0;
     wq.qn = 0;
     wq.hoff = (uint32_t)(uintptr_t)(qba_lds_u32 *)hist;
     asm("" : "+v"(wq.hoff));
-    for (uint32_t u = threadIdx.x;; u += QBA_BLOCK) {  // wave-uniform trip count
+    for (uint32_t u = (wv << 6) | __lane_id();; u += QBA_BLOCK) {  // wave-uniform trip count
       const bool act = u < nunits;
       if (!__any(act)) break;
       qba_step_l<NP, 1, SAMP, QPT, false, PK, true>(u * (4 * QPT), (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl,
                                               L, ld, hist, &wq, act);
     }
     while (wq.qn) qba_q_drain<NP, true>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
+    // the thread index rebuilt (as in qba_lists_body): nothing derived from
+    // threadIdx.x stays live across the main loop to be spilled
+    const int tid = (int)((wv << 6) | __lane_id());
     const uint32_t r0 = nunits * (4 * QPT), rq = ((uint32_t)count - r0 + 3) >> 2;
-    if (threadIdx.x < rq) {
-      const uint32_t c0 = r0 + 4 * threadIdx.x;
+    if ((uint32_t)tid < rq) {
+      const uint32_t c0 = r0 + 4 * (uint32_t)tid;
       if (c0 + 4 <= (uint32_t)count)
         qba_step_l<NP, 1, SAMP, 1, false, PK>(c0, (uint32_t)count, 0, k0, k1, ps, pat, apat, thr, pl, L, ld, hist);
       else
@@ -1710,15 +1721,15 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     }
     __syncthreads();
     int64_t *h = H + inst * C::HB, *c = Cc + inst * C::CB, *p = P + inst * C::W;
-    for (int i = threadIdx.x; i < C::HB; i += QBA_BLOCK) h[i] = qba_hval<NP>(hist, i);
-    for (int r = threadIdx.x; r < C::CB; r += QBA_BLOCK) {
+    for (int i = tid; i < C::HB; i += QBA_BLOCK) h[i] = qba_hval<NP>(hist, i);
+    for (int r = tid; r < C::CB; r += QBA_BLOCK) {
       const int u = r / (C::G * C::G), g = (r / C::G) % C::G, k = r % C::G;
       const int64_t v = g < k ? hist[C::HBL + u * C::CP + C::pidx(g, k)]
                               : g > k ? hist[C::HBL + u * C::CP + C::pidx(k, g)]
                                       : qba_psize<NP>(hist, u);
       c[r] = v;
     }
-    for (int u = threadIdx.x; u < C::W; u += QBA_BLOCK) p[u] = qba_psize<NP>(hist, u);
+    for (int u = tid; u < C::W; u += QBA_BLOCK) p[u] = qba_psize<NP>(hist, u);
     __syncthreads();
   }
 }
