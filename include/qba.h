@@ -202,8 +202,9 @@ QBA_API int qba_sample_check_packed_deferred(qba_ctx *ctx, int n_parties, uint64
  * capture of a captured pending reduction drops it (QBA_ESTATE: that call's
  * counts stay incomplete).  Counting calls of one ctx on different streams
  * share its scratch: a counting call on another stream than the previous
- * one synchronises the device first (qba_last_stats and qba_destroy flush a
- * pending reduction first). */
+ * one synchronises the device first (so do not switch a ctx's stream while
+ * another thread captures a graph on this device; qba_last_stats and
+ * qba_destroy flush a pending reduction first). */
 QBA_API int qba_flush_deferred(qba_ctx *ctx);
 /* Rows [0, rows) of `count` columns between the layouts.  pack: *bad_dev (may
  * be NULL) receives how many values were > 15 (stored as value & 15). */
