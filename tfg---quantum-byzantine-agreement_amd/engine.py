@@ -141,7 +141,7 @@ class Engine:
     def alloc_lists(self, n: int, count: int) -> torch.Tensor:
         # rows start 4 KiB-aligned: the 8-B-per-lane row stores then never
         # straddle a partial line at a row start (1.3% over 64-B alignment at
-        # n = 11, tools/exp/ldalign.sh)
+        # n = 11, measured in round 2)
         ld = max(4096, (count + 4095) // 4096 * 4096)
         return torch.empty((n + 1, ld), dtype=torch.uint8, device=self.device)
 
@@ -239,7 +239,7 @@ class Engine:
         _, w = self.sizes(n)
         # rows start 4 KiB-aligned: the 8-B-per-lane row stores then never
         # straddle a partial line at a row start (1.3% over 64-B alignment at
-        # n = 11, tools/exp/ldalign.sh)
+        # n = 11, measured in round 2)
         nb = (count + 1) // 2 if packed else count
         ld = max(4096, (nb + 4095) // 4096 * 4096)
         if lists is None:
