@@ -327,7 +327,7 @@ __device__ __forceinline__ void qba_closed_finish(const QbaClosed &c, const uint
   uint32_t qm = (uint32_t)__builtin_amdgcn_sbfe((int)c.w0, 0, 1);
   asm("" : "+v"(qm));
   // not-Q words masked by ONE shared ~qm & M4, then one v_and_or per word:
-  // D = (nq_raw & nqm) | (qm & (q ^ R))  (-0.2 VALU/entry, profiles/r3/ab32)
+  // D = (nq_raw & nqm) | (qm & (q ^ R))  (-0.2 VALU/entry, profiles/r3/ab32_microopts_and_stores.txt)
   uint32_t nqm = ~qm & F::M4;
   asm("" : "+v"(nqm));
 #pragma unroll
@@ -1046,7 +1046,7 @@ __device__ __forceinline__ void qba_step(uint32_t c0, uint32_t count, uint64_t f
 // of group 4i+g' -- BEFORE the transpose: one 4x4 transpose per 8 entries
 // (QPT = 2, one 4-B store per row) instead of two, and half the HBM writes,
 // which keeps the chip's clock up in the driver's cold window
-// (profiles/r3/ab32: 12-row packed stores 375-381 us vs 421-424 us).
+// (profiles/r3/ab32_microopts_and_stores.txt: 12-row packed stores 375-381 us vs 421-424 us).
 // QPT = 1 (unaligned starts, the tail quads): 2 bytes per row, stored as bytes
 // (a chunk may start at an odd byte).  MODE 2 reads the same layout; an
 // unpacked quad's entries come out permuted (counting is order-free).
@@ -1404,7 +1404,7 @@ __device__ __forceinline__ void qba_lists_body(const QbaProgramSet *__restrict__
   // thread index from it and the lane id instead of keeping threadIdx.x (and
   // what derives from it) live across the loop -- at 64 VGPRs those values
   // were spilled to scratch, and a kernel with scratch waits ~6 us longer for
-  // its dispatch after the previous kernel (profiles/r5/noscratch)
+  // its dispatch after the previous kernel (profiles/r5/slab_event)
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if constexpr (MODE != 0) {
     QbaWaveQ wq;
