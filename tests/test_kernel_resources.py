@@ -5,8 +5,8 @@ change can silently lose (profiles/r5/slab_event/):
   * no scratch: a kernel with a private segment is dispatched ~0.6 us later
     after the previous kernel, and a spill inside the main loop makes every
     step wait for all outstanding row stores;
-  * at most 64 VGPRs for the 8-wave-per-SIMD list kernels (2 workgroups of
-    1024 threads per CU).
+  * at most 64 VGPRs for the kernels compiled for 8 waves per SIMD (the
+    list kernels' 2 workgroups of 1024 threads per CU; the batched kernel).
 Read from the kernel descriptors inside libqba.so (tests/kd_util.py).
 """
 from pathlib import Path
@@ -25,7 +25,7 @@ HOT = {
     "_Z11qba_k_listsILi11ELi1ELi2ELi2ELi1ELi1EE": 64,
     "_Z17qba_k_lists_pbdefILi11ELi2ELi1EE": 64,
     "_Z15qba_k_lists_defILi11ELi2ELi2ELi1EE": None,
-    "_Z13qba_k_batchedILi7ELi2ELi2ELi1EE": None,
+    "_Z13qba_k_batchedILi7ELi2ELi2ELi1EE": 64,
 }
 
 

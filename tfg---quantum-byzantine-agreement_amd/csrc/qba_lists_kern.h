@@ -1675,8 +1675,12 @@ __global__ void QBA_LISTS_BOUNDS_PB
 // run with Philox key seed_base + i over entries [0, count).  A workgroup
 // owns whole instances, so its LDS histogram IS the instance's final count
 // and is written out directly (no slab, no reduce launch).
+// Compiled for 8 waves per SIMD on the closed sampler (configs[3]: 0.743 ->
+// 0.728 ms/step, profiles/r5/batched; 53 VGPRs once the per-instance output
+// addresses are no longer hoisted across the main loop)
 template <int NP, int SAMP, int QPT, int PK>
-__global__ void __launch_bounds__(QBA_BLOCK)
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, QBA_BLOCK),
+                               amdgpu_waves_per_eu(SAMP == QBA_S_CLOSED ? 8 : 1)))
     qba_k_batched(const QbaProgramSet *__restrict__ ps, uint64_t seed_base, int64_t n_inst,
                   uint64_t count, uint8_t *__restrict__ lists, uint64_t ld, uint64_t inst_stride,
                   int64_t *__restrict__ H, int64_t *__restrict__ Cc, int64_t *__restrict__ P) {
@@ -1710,7 +1714,8 @@ __global__ void __launch_bounds__(QBA_BLOCK)
     while (wq.qn) qba_q_drain<NP, true>(wq, hist, wq.qn < 64 ? wq.qn : 64u);  // wave-uniform
     // the thread index rebuilt (as in qba_lists_body): nothing derived from
     // threadIdx.x stays live across the main loop to be spilled
-    const int tid = (int)((wv << 6) | __lane_id());
+    int tid = (int)((wv << 6) | __lane_id());
+    asm volatile("" : "+v"(tid));  // opaque: the addresses built from it are not hoisted out of the instance loop
     const uint32_t r0 = nunits * (4 * QPT), rq = ((uint32_t)count - r0 + 3) >> 2;
     if ((uint32_t)tid < rq) {
       const uint32_t c0 = r0 + 4 * (uint32_t)tid;
