@@ -5,7 +5,7 @@
 #     bench   the driver's command (N=1, --steps 20 --warmup 5), twice
 #     long    bench.py defaults (50 + 200 launches)  c0 c1 c3 c4   bench.py --config k
 #     prof    rocprofv3 --kernel-trace --stats of the driver's command (+ tools/trace_check.py)
-#     profc1  the same for --config 1
+#     profc1  the same for --config 1        profc3  ... for --config 3
 #     pmc     tools/pmc.sh passes of the headline + tools/pmc_traffic.py -> pmc/traffic.json
 #     pmcset  copy that file to profiles/traffic_n11.json (later bench steps report its traffic)
 #     ab      tools/exp/ab.sh over the experiment builds in _build/exp (ROUNDS=2)
@@ -38,6 +38,8 @@ for s in $steps; do
           python tools/trace_check.py "$out/prof" "$out/prof_bench.json" > "$out/trace_check.txt" ;;
     profc1) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_c1" \
                -o bench -- python "$root/bench.py" --config 1 --steps 200 --no-cpu-baseline > "$out/prof_c1.log" 2>&1) ;;
+    profc3) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_c3" \
+               -o bench -- python "$root/bench.py" --config 3 --no-cpu-baseline > "$out/prof_c3.log" 2>&1) ;;
     pmc) timeout -k 10 600 bash tools/pmc.sh "gpurun_out/$tag/pmc"
          python tools/pmc_traffic.py "$out/pmc" 125000000 11 > "$out/pmc/traffic.json"
          python tools/pmc_summary.py "$out/pmc" > "$out/pmc/summary.txt" ;;
