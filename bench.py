@@ -38,13 +38,16 @@ Other BASELINE.json configs (one JSON line each, one GPU):
 
 roofline.achieved = the HBM bytes the fused pass must move per launch -- the
 lists written once ((n+1)/2 B per entry as nibble rows, (n+1) B as byte rows;
-the checks run from registers and never re-read them) -- / the launch's device
+the checks run from registers and never re-read them) -- / the step's device
 time, measured with HIP events on the stream the kernels run on; frac is that
 over the 8 TB/s peak, a physical fraction (roofline.traffic: the PMC-measured
 bytes of this build, within ~3 % of it).  BASELINE's own scoring convention
 (2(n+1) B per entry: lists written + read back once) is reported beside it as
-roofline.metric_scale.  The launch is the whole sample_check call: the fused
-kernel and the slab reduction (qba_k_reduce).  One event pair brackets the K
+roofline.metric_scale.  The step is one deferred sample_check call: the
+fused kernel, which also reduces the PREVIOUS step's counts in workgroups
+after its own (qba_k_lists_pbdef); the last step's reduction is the flush
+inside the timed region (QBA_BENCH_DEFER=0: the synchronous call, list kernel
++ qba_k_reduce per step).  One event pair brackets the K
 timed launches (device time / K): an event pair around every launch costs
 ~10 us of GPU time per step (markers between the kernels; rocprofv3 trace:
 10.4 us gaps before each list kernel, none with one pair), which would be
