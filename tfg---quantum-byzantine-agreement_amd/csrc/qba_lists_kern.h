@@ -576,7 +576,10 @@ __device__ __forceinline__ void qba_sample_quad(uint32_t c0, int valid, uint64_t
       for (int jp = 0; jp < 2; ++jp) {
         QbaClosed cl[2];
         const uint64_t p = ((uint64_t)phi << 32) | (uint64_t)(plo + (uint32_t)jp);
-        const QbaU4 x = qba_philox_k<true>(plo + (uint32_t)jp, phi, 0u, 0u, k0, k1);
+        // the 20 round keys loop-invariant in SGPRs (SGPR budget allows them
+        // since round 5: 108 instead of 158 SALU per thread-step, cycles -1 %,
+        // profiles/r5/keys_sgpr)
+        const QbaU4 x = qba_philox_k<false>(plo + (uint32_t)jp, phi, 0u, 0u, k0, k1);
         qba_closed_rank<NP>(x.x, x.y, p, 0u, k0, k1, cl[0]);
         qba_closed_rank<NP>(x.z, x.w, p, 1u, k0, k1, cl[1]);
         uint4 A[2];
