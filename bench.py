@@ -186,6 +186,49 @@ def verify_counts(n, seed, per, world, H, C, P):
     return out
 
 
+GOLDEN_ROWS = ROOT / "tests" / "golden" / "config2_rows_n11_5eed.npz"
+
+
+def device_row_sums(lists, n, count, packed):
+    """Position-weighted checksums of the rows a step wrote, computed on the
+    device from the rows as stored: int64 [n+1, 2] with, per row g,
+    (sum_k L_g[k], sum_k L_g[k] * (k+1)) over the step's columns k (nibble
+    rows: column 2b = the low nibble of byte b, 2b+1 the high one).  Outside
+    the timed region; the same sums as oracle_lib.stream_row_sums."""
+    import torch
+    g = n + 1
+    s0 = torch.zeros(g, dtype=torch.int64, device=lists.device)
+    s1 = torch.zeros(g, dtype=torch.int64, device=lists.device)
+    nb = (count + 1) // 2 if packed else count
+    step = 1 << 22
+    for off in range(0, nb, step):
+        m = min(step, nb - off)
+        x = lists[:g, off:off + m].to(torch.int64)
+        k = torch.arange(off, off + m, dtype=torch.int64, device=lists.device)
+        if packed:
+            lo, hi = x & 15, x >> 4
+            s0 += lo.sum(1) + hi.sum(1)
+            s1 += (lo * (2 * k + 1)).sum(1) + (hi * (2 * k + 2)).sum(1)
+        else:
+            s0 += x.sum(1)
+            s1 += (x * (k + 1)).sum(1)
+    return torch.stack([s0, s1], 1)
+
+
+def verify_rows(n, seed, per, sums):
+    """bench.py's row check: sums[r] (int64 [n+1, 2], rank r's device_row_sums
+    of its shard's rows) against the C twin's sums of shard r
+    (tests/golden/gen_config2_rows.py), when recorded; else {}."""
+    import numpy as np
+    if n != 11 or seed != 0x5EED or per != 125_000_000 or len(sums) > 8 or not GOLDEN_ROWS.exists():
+        return {}
+    S = np.load(GOLDEN_ROWS)["S"].astype(np.int64)
+    same = [bool(np.array_equal(np.asarray(s, dtype=np.int64), S[r])) for r, s in enumerate(sums)]
+    return {"rows_equal_golden": all(same), "rows_equal_golden_per_rank": same,
+            "rows_golden": f"C-twin row sums (sum L_g[k], sum L_g[k]*(k+1)) of every rank's shard rows "
+                           f"(tests/golden/{GOLDEN_ROWS.name})"}
+
+
 # Measured issue cost per wave64 VALU instruction on one SIMD at 8 waves
 # (tools/exp/valu_rate.hip, profiles/r4/micro/valu_rate.txt): simple ops
 # (v_add_u32 2.31, v_bitop3_b32 2.42) and the 64-bit multiply that
@@ -270,6 +313,12 @@ def headline(args):
     counts = [eng_mod.Counts(*dist_mod.split_counts(f, n)) for f in flats]
     pending = [None] * nbuf
     stream = torch.cuda.current_stream()
+    # what the collective itself saw: ones all-reduced over the same group the
+    # counts go through (RCCL under the nccl backend); must be the world size
+    ranks_seen = dist_mod.group_ranks(eng.device)
+    if ranks_seen != world:
+        raise SystemExit(f"the all-reduce summed {ranks_seen} ranks, WORLD_SIZE={world}")
+    backend = torch.distributed.get_backend() if world > 1 else None
 
     def wait_buf(b):
         if pending[b] is not None:
@@ -361,6 +410,15 @@ def headline(args):
     # verification result of the last step (the all-reduced counts): honest Q
     # positions never collide, and against the C twin's totals when recorded
     Hn, Cn, Pn = (x.cpu().numpy() for x in (H, C, P))
+    # ... and the rows it wrote (every step writes the same rows): checksums on
+    # the device, gathered from every rank
+    rs = device_row_sums(lists, n, per, packed)
+    if world > 1:
+        gathered = [torch.zeros_like(rs) for _ in range(world)]
+        torch.distributed.all_gather(gathered, rs)
+        row_sums = [x.cpu().numpy() for x in gathered]
+    else:
+        row_sums = [rs.cpu().numpy()]
     if rank != 0:
         eng.close()
         return
@@ -434,7 +492,9 @@ def headline(args):
                                      "not a physical fraction (can pass 1)"},
             "issue": issue,
         },
-        "verification": verify_counts(n, args.seed, per, world, Hn, Cn, Pn),
+        "verification": {**verify_counts(n, args.seed, per, world, Hn, Cn, Pn),
+                         **verify_rows(n, args.seed, per, row_sums),
+                         "allreduce_ranks": ranks_seen, "backend": backend},
         "rank_launch_ms": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -149,10 +149,10 @@ QBA_API int qba_check_counts(qba_ctx *ctx, int n_parties, const uint8_t *lists_d
  * check of nibble rows) whose 8-bit pair bins wrapped and that recounted
  * their entries exactly from the stored rows.  Pair-bin launches give a
  * workgroup at most 2^18 entries (a larger call is split, later parts
- * accumulating), where no bin wraps for sampled lists; the environment
- * variables the tests use to force wraps and pair bins on small launches
- * (QBA_LIST_GRID = workgroups per launch, QBA_PB_MIN_ENTRIES) keep a
- * workgroup below 2^23 entries, so a wrap is always detected exactly. */
+ * accumulating), where no bin wraps for sampled lists; the test seam that
+ * forces wraps and pair bins on small launches (qba_test_set_knobs' list_grid
+ * and pb_min_entries) gives a workgroup at most 2^23 entries per launch, below
+ * group 0's 24-bit total, so a wrap is always detected exactly. */
 QBA_API int qba_last_stats(qba_ctx *ctx, int64_t *out2_host);
 /* Fused sample + check: lists are written once and counted from registers. */
 QBA_API int qba_sample_check(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
@@ -186,7 +186,10 @@ QBA_API int qba_check_counts_packed(qba_ctx *ctx, int n_parties, const uint8_t *
  * another stream is flushed there and ordered by an event.  A pair-bin call
  * larger than one launch's per-workgroup budget (above ~1.3e8 entries at n =
  * 11) runs its earlier parts synchronously and defers only its last part's
- * reduction. */
+ * reduction; its first part flushes a pending call and then overwrites the
+ * outputs, so a pending call that shares this call's H/C/P buffers ends with
+ * this call's counts in them (as it would after any later call into the same
+ * buffers). */
 QBA_API int qba_sample_check_deferred(qba_ctx *ctx, int n_parties, uint64_t seed, uint64_t first,
                                       uint64_t count, uint8_t *lists_dev, uint64_t ld, int64_t *H_dev,
                                       int64_t *C_dev, int64_t *P_dev, int accumulate, qba_stream stream);
@@ -204,7 +207,9 @@ QBA_API int qba_sample_check_packed_deferred(qba_ctx *ctx, int n_parties, uint64
  * share its scratch: a counting call on another stream than the previous
  * one synchronises the device first (so do not switch a ctx's stream while
  * another thread captures a graph on this device; qba_last_stats and
- * qba_destroy flush a pending reduction first). */
+ * qba_destroy flush a pending reduction first).  The previous stream is known
+ * only by its handle value: synchronise a stream that ran counting calls of
+ * this ctx before destroying it, since a new stream may reuse the handle. */
 QBA_API int qba_flush_deferred(qba_ctx *ctx);
 /* Rows [0, rows) of `count` columns between the layouts.  pack: *bad_dev (may
  * be NULL) receives how many values were > 15 (stored as value & 15). */
@@ -344,6 +349,16 @@ QBA_API int qba_alias_build(const double *prob_host, int32_t k, uint64_t *thr_ho
 /* Philox4x32-10 on the device for KATs: out[4*i..] = philox(ctr_i, key). */
 QBA_API int qba_philox_dev(qba_ctx *ctx, const uint32_t *ctr_dev, int64_t n, uint64_t key,
                    uint32_t *out_dev, qba_stream stream);
+/* Test seam: the launch-shape knobs the GPU tests use to reach the list
+ * kernels' rare paths on small inputs (the library reads no environment
+ * variable).  chunk_entries: entries per list-kernel launch (0 = the shipped
+ * 2^31; else 4 .. 2^31, rounded down to a multiple of 4) -- chunk splits;
+ * pb_min_entries: launches from this many entries count n = 11 in pair bins
+ * (< 0 = the shipped 2^24); list_grid: > 0 caps the list kernels' workgroups
+ * and forces pair bins, each workgroup taking up to 2^23 entries per launch
+ * -- pair-bin wraps and their recount (0 = off).  Flushes a pending deferred
+ * reduction first.  Results are bit-identical under every setting. */
+QBA_API int qba_test_set_knobs(qba_ctx *ctx, uint64_t chunk_entries, int64_t pb_min_entries, int list_grid);
 
 #ifdef __cplusplus
 }

@@ -106,6 +106,26 @@ def stream_counts(n: int, seed: int, first: int, count: int, prog_notq: dict, pr
     return H, Cc, P, int(bad)
 
 
+def stream_row_sums(n: int, seed: int, first: int, count: int, prog_notq: dict, prog_q: dict,
+                    closed: bool = False) -> np.ndarray:
+    """uint64 [n+1, 2]: per row g, (sum_k L_g[k], sum_k L_g[k] * (k+1)) over the
+    lists of entries [first, first+count), k counted from 0 at `first`;
+    sampled without storing the lists (any size)."""
+    S = np.zeros((n + 1, 2), np.uint64)
+    k0, a0 = _prog_args(prog_notq)
+    k1, a1 = _prog_args(prog_q)
+    lib().oracle_stream_row_sums(C.c_int(n), C.c_uint64(seed), C.c_uint64(first), C.c_uint64(count),
+                                 C.c_int(int(closed)), *a0, *a1, _p(S))
+    return S
+
+
+def row_sums(lists: np.ndarray) -> np.ndarray:
+    """The same checksum of lists held in memory (uint8 [rows, count])."""
+    L = np.asarray(lists, dtype=np.uint64)
+    k = np.arange(1, L.shape[1] + 1, dtype=np.uint64)
+    return np.stack([L.sum(1), (L * k).sum(1)], axis=1).astype(np.uint64)
+
+
 def batched_counts(n: int, seed_base: int, n_inst: int, count: int, prog_notq: dict, prog_q: dict,
                    closed: bool = False):
     """Per-instance H, C, P of n_inst independent runs (key seed_base + i,

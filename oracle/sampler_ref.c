@@ -411,6 +411,36 @@ void oracle_batched_counts(int n, uint64_t seed_base, int64_t n_inst, uint64_t c
   }
 }
 
+/* Position-weighted row checksums of the lists of entries [first, first+count)
+ * without storing them: S[2g] = sum_k L_g[k], S[2g+1] = sum_k L_g[k] * (k+1)
+ * (k the column within the call; unsigned 64-bit, which never wraps below
+ * 2^54 columns at w <= 16).  Layout-free: bench.py computes the same sums on
+ * the device from the nibble rows it wrote. */
+void oracle_stream_row_sums(int n, uint64_t seed, uint64_t first, uint64_t count, int closed, int nfac0,
+                            const int32_t *desc0, const uint64_t *pat0, const uint64_t *apat0,
+                            const uint64_t *thr0, int nfac1, const int32_t *desc1, const uint64_t *pat1,
+                            const uint64_t *apat1, const uint64_t *thr1, uint64_t *S) {
+  const prog_t p0 = {nfac0, desc0, pat0, apat0, thr0}, p1 = {nfac1, desc1, pat1, apat1, thr1};
+  const uint64_t t = perm_threshold(n);
+  const int G = n + 1;
+  memset(S, 0, 2 * (size_t)G * sizeof(uint64_t));
+#pragma omp parallel
+  {
+    uint64_t s[32] = {0};
+    uint8_t vals[16];
+#pragma omp for schedule(static)
+    for (int64_t k = 0; k < (int64_t)count; ++k) {
+      entry_values(n, seed, first + (uint64_t)k, closed, &p0, &p1, t, vals);
+      for (int g = 0; g < G; ++g) {
+        s[2 * g] += vals[g];
+        s[2 * g + 1] += (uint64_t)vals[g] * (uint64_t)(k + 1);
+      }
+    }
+#pragma omp critical
+    for (int i = 0; i < 2 * G; ++i) S[i] += s[i];
+  }
+}
+
 int oracle_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

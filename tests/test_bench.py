@@ -64,6 +64,10 @@ def test_bench_self_launch_two_ranks_gpu():
     # prefix of configs[2]); at 8 ranks the same check is counts_equal_1e9_golden
     assert v["counts_equal_golden"] is True, v
     assert "counts_equal_1e9_golden" not in v
+    # the rows both ranks wrote, checksummed on the device, and the number of
+    # ranks the all-reduce itself summed
+    assert v["rows_equal_golden"] is True and v["rows_equal_golden_per_rank"] == [True, True], v
+    assert v["allreduce_ranks"] == 2 and v["backend"] == "gloo", v
     rl = line["rank_launch_ms"]
     assert len(rl["per_rank"]) == 2 and 0 < rl["min"] <= rl["max"]
 
@@ -104,3 +108,67 @@ def test_config2_totals_fixture_matches_c_twin_shard0():
     H, C, P, bad = oracle_lib.stream_counts(11, 0x5EED, 0, 125_000_000, empty, empty, closed=True)
     assert bad == 0
     assert np.array_equal(H, z["H_1"]) and np.array_equal(C, z["C_1"]) and np.array_equal(P, z["P_1"])
+
+
+def _bench_mod():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+@pytest.mark.parametrize("count", [1, 2, 4099, 100_003])
+def test_row_sums_of_stored_rows_match_c_twin(count):
+    """bench.device_row_sums (run here on CPU tensors; on the GPU over the
+    rows the timed kernel wrote) from nibble rows and from byte rows equals
+    the C twin's streamed checksum of the same entries, odd counts included."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_lib
+    b = _bench_mod()
+    empty = {"nfac": 0, "desc": np.zeros((16, 6), np.int32), "pat": np.zeros(1, np.uint64),
+             "apat": np.zeros(1, np.uint64), "thr": np.zeros(1, np.uint64)}
+    n, seed, first = 11, 0x5EED, 6 * 125_000_000 + 10
+    L = oracle_lib.sample(n, seed, first, count, empty, empty, True)
+    want = oracle_lib.stream_row_sums(n, seed, first, count, empty, empty, True)
+    assert np.array_equal(oracle_lib.row_sums(L), want)
+    nb = (count + 1) // 2
+    pk = np.zeros((n + 1, nb + 7), np.uint8)
+    pk[:, : count // 2] = L[:, 0:count - count % 2:2] | (L[:, 1::2][:, : count // 2] << 4)
+    if count % 2:
+        pk[:, nb - 1] = L[:, -1]
+    got = b.device_row_sums(torch.from_numpy(pk), n, count, True).numpy()
+    assert np.array_equal(got, want.astype(np.int64))
+    byte = np.zeros((n + 1, count + 5), np.uint8)
+    byte[:, :count] = L
+    assert np.array_equal(b.device_row_sums(torch.from_numpy(byte), n, count, False).numpy(), want.astype(np.int64))
+
+
+def test_row_golden_verification_cpu():
+    """bench.verify_rows: the recorded shards pass, one changed sum fails,
+    other workloads report nothing."""
+    import numpy as np
+    b = _bench_mod()
+    S = np.load(ROOT / "tests" / "golden" / "config2_rows_n11_5eed.npz")["S"].astype(np.int64)
+    for world in (1, 2, 4, 8):
+        v = b.verify_rows(11, 0x5EED, 125_000_000, [S[r] for r in range(world)])
+        assert v["rows_equal_golden"] is True and v["rows_equal_golden_per_rank"] == [True] * world
+    bad = [S[0], S[1].copy()]
+    bad[1][7, 1] += 1
+    v = b.verify_rows(11, 0x5EED, 125_000_000, bad)
+    assert v["rows_equal_golden"] is False and v["rows_equal_golden_per_rank"] == [True, False]
+    assert b.verify_rows(11, 1, 125_000_000, [S[0]]) == {}
+
+
+def test_config2_rows_fixture_matches_c_twin_last_shard():
+    """The row fixture's shard 7 (entries [8.75e8, 1e9)) recomputed by the C twin."""
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_lib
+    empty = {"nfac": 0, "desc": np.zeros((16, 6), np.int32), "pat": np.zeros(1, np.uint64),
+             "apat": np.zeros(1, np.uint64), "thr": np.zeros(1, np.uint64)}
+    S = np.load(ROOT / "tests" / "golden" / "config2_rows_n11_5eed.npz")["S"]
+    assert np.array_equal(oracle_lib.stream_row_sums(11, 0x5EED, 7 * 125_000_000, 125_000_000, empty, empty, True),
+                          S[7])

@@ -42,6 +42,7 @@ def _worker(rank, world, port, lists, n, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     d.init("gloo")
+    assert d.group_ranks() == world  # what bench.py reports as verification.allreduce_ranks
     first, cnt = d.shard_bounds(lists.shape[1], rank, world)
     H, C, P = orc.counts(lists[:, first:first + cnt], n)
     flat = torch.from_numpy(np.concatenate([H.ravel(), C.ravel(), P.ravel()]).copy())
@@ -115,6 +116,7 @@ def _countparty_worker(rank, world, port, spec, out_q, hip=False):
     # device 0 (a one-GPU rehearsal of the GPU-owner layout), reduced over gloo
     eng = importlib.import_module(f"{pkg}.engine").Engine(0) if hip else OracleEngine()
     counter = countmode.ShardCounter(eng, rank, world, countmode.torch_allreduce, owners={0})
+    assert counter.check_group() == world  # tfg.py's torchrun branch does the same
     n, sizeL, ndis, seed, lists = spec
     if rank == 0:
         run = protocol.run_local(n, sizeL, ndis, eng, seed=seed, lists=lists, timeout=60,
@@ -216,6 +218,21 @@ def _failing_owner_worker(rank, world, port, out_q):
     except Exception as e:  # noqa: BLE001
         out_q.put((rank, type(e).__name__ + ": " + str(e)))
     dist.destroy_process_group()
+
+
+def test_shard_counter_check_group_refuses_a_wrong_rank_count():
+    """an all-reduce that sums another number of owners than
+    the counter's world (a communicator formed over the wrong ranks) raises
+    before any count pass; the right count passes and is returned."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent))
+    from oracle_engine import OracleEngine
+    countmode, qe = sub("countmode"), sub("_lib").QbaError
+    assert countmode.ShardCounter(OracleEngine(), 0, 3, lambda x: np.asarray(x) * 3).check_group() == 3
+    with pytest.raises(qe, match="summed 2 owner"):
+        countmode.ShardCounter(OracleEngine(), 0, 3, lambda x: np.asarray(x) * 2).check_group()
+    assert sub("distributed").group_ranks() == 1  # no process group: one rank
 
 
 def test_shard_counter_failure_raises_on_every_owner():

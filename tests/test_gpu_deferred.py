@@ -90,7 +90,7 @@ def test_deferred_mixed_with_sync_calls_and_n(engine):
     assert _eq(f, _ref_counts(engine, 11, 6, 0, 33_333))
 
 
-def test_deferred_full_chip_fallback_and_chunks(monkeypatch):
+def test_deferred_full_chip_fallback_and_chunks():
     """A launch whose list workgroups fill every resident slot takes the
     synchronous path (the pending call is flushed first); a chunked deferred
     call defers chunk by chunk (each later chunk reduces the one before)."""
@@ -107,8 +107,7 @@ def test_deferred_full_chip_fallback_and_chunks(monkeypatch):
         assert _eq(b, _ref_counts(eng, n, 43, 0, 50_000))
     finally:
         eng.close()
-    monkeypatch.setenv("QBA_CHUNK_ENTRIES", "40004")
-    eng = sub("engine").Engine(0)
+    eng = sub("engine").Engine(0).set_test_knobs(chunk=40004)
     try:
         c = _call(eng, True, 11, 44, 999, 160_021)
         d = _call(eng, False, 11, 45, 1000, 120_013)
@@ -232,11 +231,11 @@ def test_deferred_pairbin_tail_chain(engine, packed):
 
 
 @pytest.mark.parametrize("packed", [True, False])
-def test_deferred_pairbin_tail_forced_small(monkeypatch, packed):
+def test_deferred_pairbin_tail_forced_small(packed):
     """The tail-deferred pair-bin kernel forced on small, ragged calls
-    (QBA_PB_MIN_ENTRIES=0): a chain of deferred calls, one accumulating."""
-    monkeypatch.setenv("QBA_PB_MIN_ENTRIES", "0")
-    eng = sub("engine").Engine(0)
+    (pb_min = 0, qba_test_set_knobs): a chain of deferred calls, one
+    accumulating."""
+    eng = sub("engine").Engine(0).set_test_knobs(pb_min=0)
     try:
         n = 11
         calls = [(61, 0, 1), (62, 3, 4099), (63, 10, 250_001), (64, 0, 1_000_000)]
@@ -251,3 +250,68 @@ def test_deferred_pairbin_tail_forced_small(monkeypatch, packed):
         assert _eq(acc, _ref_counts(eng, n, 65, 0, 100_001))
     finally:
         eng.close()
+
+
+def _bench():
+    import importlib.util
+    from conftest import ROOT
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+def _rows_window(p, start, count):
+    """Columns [start, start+count) of nibble rows p (device), unpacked on the host."""
+    b0, b1 = start // 2, (start + count + 1) // 2
+    u = sub("engine").unpack_nibbles(p[:, b0:b1].cpu().numpy(), 2 * (b1 - b0))
+    return u[:, start - 2 * b0:start - 2 * b0 + count]
+
+
+@pytest.mark.parametrize("seed,first,count,golden_shard", [
+    (77, 1000, (1 << 24) + 12_345, None),          # >= 2^24: qba_k_lists_pbdef<11,2,1>, ragged tail
+    (0x5EED, 0, 125_000_000, 0),                    # the bench step itself (rank 0's shard)
+    (0x5EED, 5 * 125_000_000, 125_000_000, 5),      # rank 5's shard of sizeL = 1e9
+])
+def test_deferred_pairbin_rows_bit_exact(engine, seed, first, count, golden_shard):
+    """the ROWS the timed kernel writes.  bench.py times
+    qba_sample_check_packed_deferred at >= 2^24 entries, i.e. the pair-bin
+    kernel with the previous call's reduction in its tail (qba_k_lists_pbdef).
+    A deferred call runs first, so that reduction is live; then the rows of
+    the big call are compared with the C twin (oracle_lib.sample, tfg.py:
+    68-84, 128-129) over its first and last 4,099 entries and three windows
+    inside, and their device checksums (bench.device_row_sums, every entry)
+    with the C twin's -- at the bench's size with the recorded fixture of
+    that shard (tests/golden/gen_config2_rows.py).  The counts of both calls
+    are checked too (the pending call's against the C twin, the big call's
+    against the configs[2] totals where recorded)."""
+    n = 11
+    info = engine.prepare(n)
+    prior = _call(engine, True, n, 4242, 0, 20_000_000)            # pending reduction
+    p, c = engine.sample_check_packed(n, seed, first, count, deferred=True)
+    _call(engine, True, n, 4343, 0, 60_000)                          # reduces the big call
+    engine.flush_deferred()
+    torch.cuda.synchronize()
+    assert list(engine.last_stats()) == [0, 0]
+    rng = np.random.default_rng(count)
+    starts = [0, count - 4099] + sorted(int(x) for x in rng.integers(4099, count - 70_000, 3))
+    for s in starts:
+        m = 4099 if s in (0, count - 4099) else 65_537
+        ref = oracle_lib.sample(n, seed, first + s, m, info["notq"], info["q"], info["closed"])
+        assert np.array_equal(_rows_window(p, s, m), ref), (first, s, m)
+    sums = _bench().device_row_sums(p, n, count, True).cpu().numpy()
+    if golden_shard is None:
+        want = oracle_lib.stream_row_sums(n, seed, first, count, info["notq"], info["q"], info["closed"])
+    else:
+        from conftest import GOLDEN
+        want = np.load(GOLDEN / "config2_rows_n11_5eed.npz")["S"][golden_shard]
+    assert np.array_equal(sums, want.astype(np.int64))
+    assert _eq(prior, _stream_ref(engine, n, 4242, 0, 20_000_000))
+    if golden_shard is None:
+        assert _eq(c, _stream_ref(engine, n, seed, first, count))
+    elif golden_shard == 0:
+        from conftest import GOLDEN
+        z = np.load(GOLDEN / "config2_totals_n11_5eed.npz")
+        assert _eq(c, (z["H_1"], z["C_1"], z["P_1"]))
+    del p
+    torch.cuda.empty_cache()

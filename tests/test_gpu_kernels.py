@@ -486,12 +486,11 @@ def test_general_program_path(engine):
         engine.prepare(n, perm=list(range(1, n + 1)))
 
 
-def test_chunked_launches(monkeypatch):
+def test_chunked_launches():
     """Launches are split into chunks of QBA_CHUNK entries (2^31; 32-bit
     in-kernel offsets and u32 bins).  With a small chunk forced through the
-    environment, lists and counts must not change."""
-    monkeypatch.setenv("QBA_CHUNK_ENTRIES", "40000")
-    eng = sub("engine").Engine(0)
+    test seam (qba_test_set_knobs), lists and counts must not change."""
+    eng = sub("engine").Engine(0).set_test_knobs(chunk=40000)
     try:
         n, seed, first, count = 11, 31337, 999, 123_457
         info = eng.prepare(n)

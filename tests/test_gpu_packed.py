@@ -70,12 +70,11 @@ def test_packed_tiny_and_ragged(engine, count):
 
 
 @pytest.mark.parametrize("first", [999, 1000])
-def test_packed_chunked_and_unaligned_chunk_starts(monkeypatch, first):
-    """QBA_CHUNK_ENTRIES = 40004: every chunk after the first starts at byte
+def test_packed_chunked_and_unaligned_chunk_starts(first):
+    """Chunks of 40004 entries (qba_test_set_knobs): every chunk after the first starts at byte
     20002 * k, off the wide step's 4-byte alignment every other chunk, so the
     one-quad (byte-store) step runs for the cut and the wide one after it."""
-    monkeypatch.setenv("QBA_CHUNK_ENTRIES", "40004")
-    eng = sub("engine").Engine(0)
+    eng = sub("engine").Engine(0).set_test_knobs(chunk=40004)
     try:
         n, seed, count = 11, 31337, 160_021
         ref = _ref(eng, n, seed, first, count)
@@ -196,14 +195,13 @@ def test_packed_batched_instances(engine, n, count):
 
 
 @pytest.mark.parametrize("packed", [True, False])
-def test_pairbin_wrap_recount_exact(monkeypatch, packed):
+def test_pairbin_wrap_recount_exact(packed):
     """The fused n = 11 kernel counts in 8-bit pair bins (qba_lists_kern.h,
-    QbaPB).  QBA_LIST_GRID = 2 puts ~2e6 entries on each of two workgroups, so
+    QbaPB).  list_grid = 2 (qba_test_set_knobs) puts ~2e6 entries on each of two workgroups, so
     every pair bin wraps many times; the flush's lane-total test must see it
     and the workgroups recount their rows exactly (stats[1] = 2).  Lists and
     counts stay bit-exact against the C twin, for both row layouts."""
-    monkeypatch.setenv("QBA_LIST_GRID", "2")
-    eng = sub("engine").Engine(0)
+    eng = sub("engine").Engine(0).set_test_knobs(list_grid=2)
     try:
         n, seed, first, count = 11, 0xBADC0DE, 6, 4_000_003
         ref = _ref(eng, n, seed, first, count)
@@ -255,9 +253,9 @@ def _collided(n, count, seed):
     return L
 
 
-@pytest.mark.parametrize("force,count", [("QBA_PB_MIN_ENTRIES=0", 30_001), ("QBA_PB_MIN_ENTRIES=0", 8),
-                                         ("QBA_PB_MIN_ENTRIES=0", 1_000_003), ("QBA_LIST_GRID=2", 5_000_001)])
-def test_pairbin_check_counts_collisions_exact(monkeypatch, force, count):
+@pytest.mark.parametrize("force,count", [("pb_min=0", 30_001), ("pb_min=0", 8),
+                                         ("pb_min=0", 1_000_003), ("list_grid=2", 5_000_001)])
+def test_pairbin_check_counts_collisions_exact(force, count):
     """Cond3 (tfg.py:96-98) through the pair-bin counter: qba_check_counts_packed
     at n = 11 counts in pair bins (QbaUsePB), so injected equal pairs drive the
     counter's distinctness test and its equal-pair slow path (C[u][g][h] in B's
@@ -266,8 +264,7 @@ def test_pairbin_check_counts_collisions_exact(monkeypatch, force, count):
     bit-exact against the numpy restatement; uniform lists over [0, 4) make
     every Q entry collide."""
     key, val = force.split("=")
-    monkeypatch.setenv(key, val)
-    eng = sub("engine").Engine(0)
+    eng = sub("engine").Engine(0).set_test_knobs(**{key: int(val)})
     try:
         n = 11
         for L in (_collided(n, count, count), np.random.default_rng(5).integers(0, 4, (n + 1, count)).astype(np.uint8)):
@@ -280,7 +277,7 @@ def test_pairbin_check_counts_collisions_exact(monkeypatch, force, count):
             offdiag = int(C.sum() - sum(C[:, g, g].sum() for g in range(n + 1)))
             assert offdiag > 0 or count < 64
             st = list(eng.last_stats())
-            assert st == ([0, 2] if key == "QBA_LIST_GRID" else [0, 0]), st
+            assert st == ([0, 2] if key == "list_grid" else [0, 0]), st
     finally:
         eng.close()
 
@@ -316,13 +313,12 @@ def test_slab_event_survives_stream_destruction(engine):
 
 
 @pytest.mark.parametrize("packed", [True, False])
-def test_pairbin_kernel_small_launches_bit_exact(monkeypatch, packed):
+def test_pairbin_kernel_small_launches_bit_exact(packed):
     """The pair-bin kernel (picked for launches of >= 2^24 entries) forced on
-    small and ragged launches with QBA_PB_MIN_ENTRIES=0: tails (partial quads,
+    small and ragged launches with pb_min = 0 (qba_test_set_knobs): tails (partial quads,
     counted entry by entry into the pair bins), odd first columns and a
     chunked call, bit-exact against the C twin, no recount."""
-    monkeypatch.setenv("QBA_PB_MIN_ENTRIES", "0")
-    eng = sub("engine").Engine(0)
+    eng = sub("engine").Engine(0).set_test_knobs(pb_min=0)
     try:
         n = 11
         for first, count in [(0, 1), (0, 2), (3, 5), (0, 8), (1, 17), (10, 4099), (0, 100_003), (7, 2_000_001)]:

@@ -14,7 +14,7 @@ from scipy import stats
 import oracle_lib
 import statevector as sv_oracle
 import tfg_oracle as orc
-from conftest import GOLDEN, ROOT, sub
+from conftest import GOLDEN, PKG_NAME, ROOT, sub
 
 KATS = [  # Random123 philox4x32-10 known answers
     ([0, 0, 0, 0], 0, [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]),
@@ -165,6 +165,19 @@ def test_library_exports_every_declared_symbol():
         assert name in lib_mod.SIGNATURES, name
     assert set(lib_mod.SIGNATURES) == set(declared)
     assert lib.qba_version() >= 100
+
+
+def test_shipped_library_reads_no_environment_knob():
+    """the launch-shape knobs the GPU tests use (chunk size,
+    pair-bin threshold, grid cap) reach the library only through
+    qba_test_set_knobs; the shipped library reads no environment variable, so
+    a stray variable cannot change kernel selection in production."""
+    blob = Path(sub("_lib").LIB_PATH).read_bytes()
+    for name in (b"QBA_LIST_GRID", b"QBA_PB_MIN_ENTRIES", b"QBA_CHUNK_ENTRIES"):
+        assert name not in blob, name
+    csrc = ROOT / PKG_NAME / "csrc"
+    for f in sorted(csrc.glob("*.hip")) + sorted(csrc.glob("*.cpp")) + sorted(csrc.glob("*.h")):
+        assert "getenv" not in f.read_text(), f.name
 
 
 def test_shipped_library_has_no_experiment_switch():

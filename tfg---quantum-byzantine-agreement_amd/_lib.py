@@ -77,6 +77,7 @@ SIGNATURES = {
     "qba_values_to_bits": [_p, _p, _u64, C.c_int, _p, _p],
     "qba_alias_build": [_pf64, _i32, _pu64, _pi32],
     "qba_philox_dev": [_p, _p, _i64, _u64, _p, _p],
+    "qba_test_set_knobs": [_p, _u64, _i64, C.c_int],
 }
 _RESTYPE = {"qba_last_error": C.c_char_p}
 

@@ -97,6 +97,27 @@ class ShardCounter:
         self.allreduce = allreduce
         self._owners = owners
 
+    def group_ranks(self) -> int:
+        """A one-element int64 1 from every owner through this counter's own
+        all-reduce (RCCL, torch.distributed or the test's MPI seam): how many
+        owners the collective summed."""
+        dev = getattr(self.engine, "device", None)
+        if dev is not None:
+            import torch
+            one = torch.ones(1, dtype=torch.int64, device=dev)
+        else:
+            one = np.ones(1, np.int64)
+        return int(np.asarray(self.allreduce(one)).reshape(-1)[0])
+
+    def check_group(self) -> int:
+        """group_ranks(), raising QbaError unless it is the owner count (a
+        collective: every owner calls it, right after the group is formed)."""
+        seen = self.group_ranks()
+        if seen != self.world:
+            from ._lib import QbaError
+            raise QbaError(f"the count all-reduce summed {seen} owner(s), expected {self.world}")
+        return seen
+
     def participates(self, party_rank: int) -> bool:
         return party_rank in self._owners if self._owners is not None else party_rank < self.world
 

@@ -43,15 +43,6 @@ extern "C" int qba_init(int device, qba_ctx **out) {
   qba_ctx *ctx = new qba_ctx();
   ctx->device = device;
   ctx->num_cus = prop.multiProcessorCount;
-  if (const char *c = getenv("QBA_CHUNK_ENTRIES")) {
-    const unsigned long long v = strtoull(c, nullptr, 10) & ~3ull;
-    if (v >= 4 && v <= QBA_CHUNK) ctx->chunk = v;
-  }
-  if (const char *c = getenv("QBA_PB_MIN_ENTRIES")) ctx->pb_min = strtoull(c, nullptr, 10);  // tests
-  if (const char *c = getenv("QBA_LIST_GRID")) {  // tests: force many entries per workgroup
-    const long v = strtol(c, nullptr, 10);
-    if (v > 0 && v < (1l << 20)) ctx->list_grid = (int)v;
-  }
   if (hipMalloc(&ctx->flag, 64) != hipSuccess || hipMalloc(&ctx->count1, 64) != hipSuccess ||
       hipMalloc(&ctx->stats, 64) != hipSuccess || hipMemset(ctx->stats, 0, 64) != hipSuccess) {
     qba_destroy(ctx);
@@ -63,6 +54,24 @@ extern "C" int qba_init(int device, qba_ctx **out) {
 
 // qba_lists.hip; absent from the host-only sanitizer build (no list kernels)
 extern "C" __attribute__((weak)) int qba_flush_deferred(qba_ctx *ctx);
+
+// Test seam (include/qba.h): the launch-shape knobs the GPU tests use to
+// drive chunk splits, pair bins on small launches and pair-bin wraps.  The
+// library never reads them from the environment; a ctx nobody calls this on
+// runs the shipped selection.
+extern "C" int qba_test_set_knobs(qba_ctx *ctx, uint64_t chunk_entries, int64_t pb_min_entries, int list_grid) {
+  if (!ctx || chunk_entries > QBA_CHUNK || (chunk_entries && chunk_entries < 4) || list_grid < 0 ||
+      list_grid >= (1 << 20))
+    return qba_fail(QBA_EINVAL, "qba_test_set_knobs: bad arguments");
+  int rc = qba_set_device(ctx);
+  if (rc) return rc;
+  // a pending deferred reduction was recorded under the old launch shape
+  if (ctx->pend.flush && qba_flush_deferred && (rc = qba_flush_deferred(ctx))) return rc;
+  ctx->chunk = chunk_entries ? (chunk_entries & ~3ull) : QBA_CHUNK;
+  ctx->pb_min = pb_min_entries < 0 ? QBA_PB_MIN_DEFAULT : (uint64_t)pb_min_entries;
+  ctx->list_grid = list_grid;
+  return QBA_OK;
+}
 
 extern "C" int qba_destroy(qba_ctx *ctx) {
   if (!ctx) return QBA_OK;

@@ -31,6 +31,7 @@
 #define QBA_LBLOCK 1024      // threads per workgroup of the streaming list kernels (2 per CU at n = 11)
 #define QBA_DBLOCK 768       // ... of the deferred-reduction list kernel (small launches)
 #define QBA_CHUNK (1ull << 31)  // entries per list-kernel launch (32-bit offsets, u32 bins)
+#define QBA_PB_MIN_DEFAULT (1ull << 24)  // entries from which the fused n = 11 kernel counts in pair bins
 #define QBA_EPT 4            // entries per thread per step: one dword per list row
 
 // ---------------------------------------------------------------------------
@@ -179,7 +180,7 @@ struct qba_ctx {
   int32_t *flag = nullptr;  // 1-word device flag
   int64_t *count1 = nullptr; // 1-word device counter
   int64_t *stats = nullptr;  // [2]: last counts launch: Q entries with a value >= w, spare
-  uint64_t chunk = QBA_CHUNK;  // entries per list-kernel launch (env QBA_CHUNK_ENTRIES, tests)
+  uint64_t chunk = QBA_CHUNK;  // entries per list-kernel launch (qba_test_set_knobs may lower it)
   // pinned host + device staging of the synchronous *_host entry points
   void *zc = nullptr;     // zero-copy staging: coherent pinned host memory the kernels read / write
   void *zc_d = nullptr;   // its device address
@@ -203,8 +204,9 @@ struct qba_ctx {
   // RCCL communicator of the GPU-owner ranks (qba_rccl_init), or null
   void *rccl_comm = nullptr;
   int rccl_ranks = 0;
-  int list_grid = 0;  // > 0: cap on the list kernels' workgroups, no per-workgroup budget (env QBA_LIST_GRID, tests)
-  uint64_t pb_min = 1ull << 24;  // entries from which the fused n = 11 kernel counts in pair bins (env QBA_PB_MIN_ENTRIES)
+  // test seam (qba_test_set_knobs); the shipped selection otherwise:
+  int list_grid = 0;  // > 0: cap on the list kernels' workgroups, pair bins at any size, <= 2^23 entries each
+  uint64_t pb_min = QBA_PB_MIN_DEFAULT;  // entries from which the fused n = 11 kernel counts in pair bins
   // graph capture of the pending deferred reduction (pend): 1 when it was
   // recorded inside a capture, with that capture's id
   int pend_captured = 0;

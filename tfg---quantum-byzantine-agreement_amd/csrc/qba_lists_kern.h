@@ -766,9 +766,12 @@ __device__ __forceinline__ void qba_q_push(QbaWaveQ &q, const uint32_t (&D)[CF<N
 // with the classic 32-bit bins (qba_lists_body) -- exact in every case.
 // The launcher keeps a workgroup at <= QBA_PB_BUDGET entries per launch, so
 // for sampled lists a wrap needs a bin ~18 sigma above its mean and never
-// happens in practice (tests force it with QBA_LIST_GRID).
+// happens in practice (tests force it through qba_test_set_knobs' list_grid).
 // ---------------------------------------------------------------------------
 #define QBA_PB_BUDGET (1u << 18)  // entries per workgroup per launch (wrap-free in practice)
+#define QBA_PB_FORCED_LOG2 23     // entries per workgroup (log2) under the tests' list_grid knob
+// group 0's total sits in 24-bit lanes: every workgroup must count < 2^24 entries
+static_assert(QBA_PB_BUDGET < (1u << 24) && QBA_PB_FORCED_LOG2 < 24, "pair-bin group-0 total is 24 bits");
 struct QbaPB {
   static constexpr int WORDS = 8192;       // A [4096] then B [4096]
   static constexpr int BOFF = 4096;        // B, in words
@@ -1897,8 +1900,8 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   // the fused closed-form kernel and the check of nibble rows count with
   // pair bins (QbaPB, n = 11) when the launch is large enough to repay their
   // flush (a fixed ~2 us per launch: 1e6 entries 17.7 vs 15.0 us, 1.25e8
-  // entries 298 vs 313 us, profiles/r4/small_launch); QBA_LIST_GRID (tests)
-  // forces them
+  // entries 298 vs 313 us, profiles/r4/small_launch); the tests' list_grid
+  // knob (qba_test_set_knobs) forces them
   const bool pb = ((L.mode == 1 && QbaUsePB<NP, 1, QBA_S_CLOSED, 0>::value && samp == QBA_S_CLOSED) ||
                    (L.mode == 2 && QbaUsePB<NP, 2, QBA_S_GENERAL, 1>::value && L.packed)) &&
                   (L.count >= ctx->pb_min || ctx->list_grid > 0);
@@ -1949,11 +1952,12 @@ int qba_launch_lists(qba_ctx *ctx, const QbaLaunch &L) {
   if (lds > 65536) QBA_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int cap = 0;
   int grid = grid_for(ctx, kern, lds, L.count, wide ? (L.packed ? 2 : QBA_GRID_QPT) : 1, &cap);
-  if (ctx->list_grid > 0 && grid > ctx->list_grid) grid = ctx->list_grid;  // tests (QBA_LIST_GRID)
+  if (ctx->list_grid > 0 && grid > ctx->list_grid) grid = ctx->list_grid;  // tests (qba_test_set_knobs)
   // pair bins: at most QBA_PB_BUDGET entries per workgroup and launch (QbaPB;
-  // a grid capped by QBA_LIST_GRID -- tests that force wraps -- at most 2^23,
-  // so group 0's 24-bit total stays exact)
-  const uint64_t pb_part = ctx->list_grid ? (uint64_t)grid << 23 : (uint64_t)cap * QBA_PB_BUDGET;
+  // a grid capped by the tests' list_grid knob -- tests that force wraps --
+  // at most 2^23, so group 0's 24-bit total, which counts every entry of the
+  // workgroup once, stays exact)
+  const uint64_t pb_part = ctx->list_grid ? (uint64_t)grid << QBA_PB_FORCED_LOG2 : (uint64_t)cap * QBA_PB_BUDGET;
   if (pb && L.count > pb_part) {
     // later parts accumulate; part boundaries are multiples of 2^18 entries,
     // so the row alignment and the pair parity of `first` are those of the

@@ -46,6 +46,18 @@ def init(backend: Optional[str] = None) -> Tuple[int, int, int]:
     return rank, local, world
 
 
+def group_ranks(device=None) -> int:
+    """How many ranks the collective itself sums: a one-element int64 1 from
+    every rank, all-reduced over the default group (RCCL under the "nccl"
+    backend).  1 without a process group.  A line that reports N ranks
+    proves with it that the all-reduce its counts went through saw N."""
+    if not (torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1):
+        return 1
+    one = torch.ones(1, dtype=torch.int64, device=device)
+    torch.distributed.all_reduce(one, op=torch.distributed.ReduceOp.SUM)
+    return int(one.item())
+
+
 def allreduce_counts(flat: torch.Tensor) -> torch.Tensor:
     """Sum the flat int64 [H | C | P] buffer over ranks, in place."""
     if torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1:

@@ -554,6 +554,13 @@ class Engine:
         return idx[:k].cpu().numpy(), prob[:k].cpu().numpy()
 
     # -- test helpers -------------------------------------------------------------
+    def set_test_knobs(self, chunk: int = 0, pb_min: int = -1, list_grid: int = 0) -> "Engine":
+        """qba_test_set_knobs: launch-shape knobs for the GPU tests (0 / -1 / 0
+        = the shipped selection).  Results never change, only which kernel
+        path computes them."""
+        call("qba_test_set_knobs", self.ctx, chunk, pb_min, list_grid)
+        return self
+
     def philox(self, ctr: np.ndarray, key: int) -> np.ndarray:
         ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
         d_ctr = self.to_device(ctr.view(np.int32))

@@ -86,7 +86,9 @@ def count_owners(world, mpi, ndev: int, make_engine, link=RcclLink):
     """Count mode under mpiexec: the first G = min(ranks,
     GPUs) ranks own a GPU each (device = rank % ndev) and shard the count pass
     (countmode.ShardCounter); for G > 1 rank 0 makes the group's unique id and
-    sends it to owners 1..G-1 over MPI, and every owner joins the group.
+    sends it to owners 1..G-1 over MPI, and every owner joins the group; a
+    one-element all-reduce of ones then checks that the group sums exactly G
+    owners (ShardCounter.check_group).
     Returns (engine or None, CountParty keyword arguments).  make_engine and
     link are the seams the CPU test of G > 1 owners fills with the numpy engine
     and an all-reduce over MPI (tests/mpi_driver.py --owners)."""
@@ -102,6 +104,7 @@ def count_owners(world, mpi, ndev: int, make_engine, link=RcclLink):
         else:
             world.Recv([uid, mpi.INT], source=0, tag=RCCL_ID_TAG)
         kw["counter"] = countmode.ShardCounter(eng, rank, g, link.allreduce(eng, uid.tobytes(), g, rank))
+        kw["counter"].check_group()  # the communicator must sum exactly the G owners
     return eng, kw
 
 
@@ -150,6 +153,7 @@ def _torchrun(a, size_l, verbose, log) -> int:
     torch.distributed.broadcast(seed, 0)
     list_seed = int(seed.item())
     counter = countmode.ShardCounter(eng, rank, world, countmode.torch_allreduce, owners={0})
+    counter.check_group()
     if rank != 0:
         counter.tables(a.parties, size_l, list_seed)
         return 0
