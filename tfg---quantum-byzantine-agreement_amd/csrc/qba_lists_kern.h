@@ -827,8 +827,14 @@ __device__ __forceinline__ void qba_count_pb(uint32_t c0, uint32_t c1, uint32_t 
   // 3; c0 >> 12 -> 5, 7; c1 -> 8, 10; c1 >> 8 -> 9, 11.
   const uint32_t one = 0x00010001u;
   const uint32_t s4 = c0 >> 4;
-  uint32_t U = qba_pk_onehot(c0, one) | qba_pk_onehot(s4, one) | qba_pk_onehot(c0 >> 8, one);
-  U |= qba_pk_onehot(s4 >> 8, one) | qba_pk_onehot(c1, one) | qba_pk_onehot(c1 >> 8, one);
+  // the union as two all-VGPR v_bitop3_b32 (a | b | c) and one v_or_b32, the
+  // forms gfx950 issues at the full rate, instead of v_or + two v_or3_b32
+  // (tools/exp/valu_mix2.hip; the same cycles per launch, the driver's window
+  // -3 % in the 300-launch traces of profiles/r6/ab_cond3_bitop3)
+  uint32_t U = __builtin_amdgcn_bitop3_b32(qba_pk_onehot(c0, one), qba_pk_onehot(s4, one),
+                                           qba_pk_onehot(c0 >> 8, one), 0xFE);
+  U = __builtin_amdgcn_bitop3_b32(U, qba_pk_onehot(s4 >> 8, one), qba_pk_onehot(c1, one), 0xFE);
+  U |= qba_pk_onehot(c1 >> 8, one);
   if (__popc(qba_fold16(U)) != QCfg<NP>::G) {  // some pair collides: exact slow path
     // C[u][k] for every equal pair k = pidx(g, h): B lanes 1-3 of the word
     // (x_g = k & 15, u, x_h = u ^ (1 + k / 16)), a word no Q entry's group 0
