@@ -207,9 +207,11 @@ QBA_API int qba_sample_check_packed_deferred(qba_ctx *ctx, int n_parties, uint64
  * share its scratch: a counting call on another stream than the previous
  * one synchronises the device first (so do not switch a ctx's stream while
  * another thread captures a graph on this device; qba_last_stats and
- * qba_destroy flush a pending reduction first).  The previous stream is known
- * only by its handle value: synchronise a stream that ran counting calls of
- * this ctx before destroying it, since a new stream may reuse the handle. */
+ * qba_destroy flush a pending reduction first).  Streams are told apart by
+ * their handle values: synchronise a stream that ran counting calls of this
+ * ctx before destroying it, since a new stream may reuse the handle.  The
+ * synchronisation runs in relaxed capture mode (a graph another thread
+ * captures is left alone). */
 QBA_API int qba_flush_deferred(qba_ctx *ctx);
 /* Rows [0, rows) of `count` columns between the layouts.  pack: *bad_dev (may
  * be NULL) receives how many values were > 15 (stored as value & 15). */

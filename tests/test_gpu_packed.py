@@ -282,11 +282,13 @@ def test_pairbin_check_counts_collisions_exact(force, count):
         eng.close()
 
 
-def test_slab_event_survives_stream_destruction(engine):
+def test_slab_stream_switch_after_destruction(engine):
     """A counting call on stream A, A synchronised and destroyed, then counting
-    calls on a new stream B (and deferred ones on C): the slab's ordering event
-    was recorded on A while it existed, so no destroyed stream is touched and
-    every result stays exact (qba_slab_order)."""
+    calls (and deferred ones) on new streams B, which may reuse A's handle:
+    the library never touches a previous stream -- a counting call on another
+    stream than the previous one synchronises the device first -- and every
+    result stays exact
+    (qba_slab_order)."""
     n, seed, count = 11, 99, 200_003
     ref = _ref(engine, n, seed, 0, count)
     a = torch.cuda.Stream()
@@ -310,6 +312,37 @@ def test_slab_event_survives_stream_destruction(engine):
         gc.collect()
     p4, c4 = engine.sample_check_packed(n, seed, 0, count)
     assert _same_counts(c4, ref)
+
+
+def test_slab_stream_switch_with_work_in_flight(engine):
+    """a counting call on stream B while stream A's large counting
+    launch is still in flight (A not synchronised, then destroyed): the switch
+    synchronises the device before B's launch reuses the shared slab, so A's
+    counts and B's are both exact -- in both orders of n and size."""
+    import gc
+    n = 11
+    for big, small in [((3, 0, 20_000_003), (4, 7, 300_001)), ((5, 1, 16_777_217), (6, 0, 50_000))]:
+        a = torch.cuda.Stream()
+        with torch.cuda.stream(a):
+            pa, ca = engine.sample_check_packed(n, *big)         # left in flight
+        b = torch.cuda.Stream()
+        with torch.cuda.stream(b):
+            pb, cb = engine.sample_check_packed(n, *small)
+            pd, cd = engine.sample_check_packed(n, *small, deferred=True)
+            engine.flush_deferred()
+        del a
+        gc.collect()
+        torch.cuda.synchronize()
+        s, f, c = big
+        info = engine.prepare(n)
+        H, C, P, _ = oracle_lib.stream_counts(n, s, f, c, info["notq"], info["q"], info["closed"])
+        gH, gC, gP = ca.numpy()
+        assert np.array_equal(gH, H) and np.array_equal(gC, C) and np.array_equal(gP, P), big
+        ref = _ref(engine, n, *small)
+        assert _same_counts(cb, ref) and _same_counts(cd, ref), small
+        assert np.array_equal(_unpack(pd, small[2]), ref)
+        del pa, pb, pd
+        torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("packed", [True, False])

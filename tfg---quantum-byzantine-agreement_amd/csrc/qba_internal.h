@@ -215,7 +215,7 @@ struct qba_ctx {
   // handle as a VALUE only (compared, never passed to HIP: the stream may be
   // destroyed since); a counting launch on another stream synchronises the
   // device first
-  uintptr_t slab_last = 0;
+  unsigned long long slab_last = 0;
   bool slab_set = false;
 };
 // Capture state of a stream: 1 capturing (its capture id in *id), 0 not.

@@ -177,10 +177,24 @@ static int pend_capture_ok(qba_ctx *ctx, hipStream_t s) {
 // A stream switch is rare; an event recorded after every counting launch
 // instead put a ~6 us marker between each launch and the next on the same
 // stream (profiles/r5/slab_event).
+//
+// Streams are told apart by their handle values (hipStreamGetId, which would
+// survive a handle's reuse, is a HIP 7.1 symbol that the HIP runtime PyTorch
+// ships here lacks), so a stream must be synchronised before it is destroyed
+// if this ctx counted on it (include/qba.h; PyTorch pools its streams and
+// never destroys them).  The device synchronisation runs in relaxed capture
+// mode, so a graph that another thread captures in global mode is neither
+// invalidated nor waited for (a capture has no executing work).
+static unsigned long long stream_key(hipStream_t s) { return reinterpret_cast<uintptr_t>(s) | (1ull << 63); }
+
 int qba_slab_order(qba_ctx *ctx, hipStream_t stream) {
   unsigned long long id = 0;
-  if (ctx->slab_set && ctx->slab_last != reinterpret_cast<uintptr_t>(stream) && !qba_capture_of(stream, &id)) {
-    QBA_HIP(hipDeviceSynchronize());
+  if (ctx->slab_set && ctx->slab_last != stream_key(stream) && !qba_capture_of(stream, &id)) {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    QBA_HIP(hipThreadExchangeStreamCaptureMode(&mode));
+    const hipError_t e = hipDeviceSynchronize();
+    (void)hipThreadExchangeStreamCaptureMode(&mode);  // restore this thread's mode
+    QBA_HIP(e);
     ctx->slab_set = false;
   }
   return QBA_OK;
@@ -189,7 +203,7 @@ int qba_slab_order(qba_ctx *ctx, hipStream_t stream) {
 int qba_slab_done(qba_ctx *ctx, hipStream_t stream) {
   unsigned long long id = 0;
   ctx->slab_set = !qba_capture_of(stream, &id);
-  ctx->slab_last = reinterpret_cast<uintptr_t>(stream);
+  ctx->slab_last = stream_key(stream);
   return QBA_OK;
 }
 
