@@ -254,6 +254,13 @@ def issue_roofline(tj, entries, launch_ms):
            "valu_lane_ops_per_entry": c["SQ_INSTS_VALU"] * 64 / entries,
            "valu_insts_per_simd_cycle": valu_ipc,
            "valu_busy_frac": 2 * valu_ipc}
+    # measured, not priced: SQ_ACTIVE_INST_VALU counts the quad-cycles (4 shader
+    # cycles) in which a wave issued a VALU instruction; per SIMD over the
+    # launch's quad-cycles it is the VALU's busy fraction as the hardware saw
+    # it (every VALU instruction of this kernel occupies one quad-cycle: the
+    # count equals SQ_INSTS_VALU)
+    if "SQ_ACTIVE_INST_VALU" in c:
+        out["valu_active_frac"] = c["SQ_ACTIVE_INST_VALU"] / (1024 * cyc / 4)
     if "SQ_INSTS_VALU_INT64" in c:
         i64 = c["SQ_INSTS_VALU_INT64"]
         out["valu_busy_frac_weighted"] = ((c["SQ_INSTS_VALU"] - i64) * VALU_CYC_SIMPLE
@@ -265,13 +272,13 @@ def issue_roofline(tj, entries, launch_ms):
         out["lds_atomics_per_entry"] = c["SQ_INSTS_LDS_ATOMIC"] * 64 / entries
     if "SQ_INSTS_LDS" in c:
         out["lds_insts_per_entry"] = c["SQ_INSTS_LDS"] * 64 / entries
-    busy = {"VALU": out.get("valu_busy_frac_weighted", out["valu_busy_frac"]),
+    busy = {"VALU": out.get("valu_active_frac", out.get("valu_busy_frac_weighted", out["valu_busy_frac"])),
             "LDS": out.get("lds_active_frac", 0.0)}
     top = max(busy, key=busy.get)
     out["binds"] = (f"{top} issue ({busy[top]:.0%} busy; "
                     + ", ".join(f"{k} {v:.0%}" for k, v in busy.items() if k != top)
                     + ("): neither unit saturated, the rest is dependency latency the 8 waves per SIMD do not hide"
-                       if busy[top] < 0.8 else "): saturated"))
+                       if busy[top] < 0.8 else "): near saturation -- cycles follow the VALU instruction count"))
     return out
 
 

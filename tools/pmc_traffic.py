@@ -36,7 +36,8 @@ fetch = statistics.median(vals["FETCH_SIZE"]) * 1024 * 2
 ISSUE = ("GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_LDS_ATOMIC", "SQ_INSTS_SALU",
          "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
          "SQ_INSTS_VMEM_WR", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_INT32", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
-         "SQ_ACTIVE_INST_ANY")
+         "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_SCA",
+         "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_BRANCH")
 issue = {c: statistics.median(vals[c]) for c in ISSUE if c in vals}
 write = statistics.median(vals["WRITE_SIZE"]) * 1024
 known = (n + 1) * per // (2 if layout == "packed" else 1)
