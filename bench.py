@@ -52,6 +52,14 @@ timed launches (device time / K): an event pair around every launch costs
 ~10 us of GPU time per step (markers between the kernels; rocprofv3 trace:
 10.4 us gaps before each list kernel, none with one pair), which would be
 charged to the step.  QBA_BENCH_EVENTS=step restores the per-launch pairs.
+
+verification (outside the timed region): the all-reduced H, C, P against
+the C twin's totals of entries [0, N x 1.25e8) (counts_equal_golden; at N = 8
+counts_equal_1e9_golden), position-weighted checksums of every row each rank
+wrote, computed on the device, against the C twin's checksums of that shard
+(rows_equal_golden), and allreduce_ranks: a one-element int64 1 all-reduced
+over the counts' process group before the timing (RCCL under the nccl
+backend), which must equal N.
 """
 from __future__ import annotations
 
