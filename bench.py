@@ -489,6 +489,10 @@ def headline(args):
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            # frac is physical since round 5; BENCH_r01-r04 scored
+            # BASELINE's 2(n+1) B/entry here, now roofline.metric_scale.frac
+            "frac_convention": "physical: the bytes the pass must move (lists written once as stored) / time; "
+                               "rounds 1-4 reported BASELINE's 2(n+1) B/entry here (see metric_scale.frac)",
             "kernel": (f"qba_k_lists_pbdef<{n},*> (list kernel; the previous step's count reduction runs in "
                        "its tail)" if deferred else f"qba_k_lists<{n},1,*> + qba_k_reduce") if args.mode == "fused"
                       else f"qba_k_lists<{n},0,*> + qba_k_lists<{n},2,*> + reduce",
